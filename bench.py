@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: batched affine-gap Smith-Waterman (GASAL2 LOCAL,
+score + end positions) on MI355X, BASELINE.json config 2.
+
+A step = one pass of the HIP engine over one batch of 1M synthetic pairs
+(ql = tl = 150, SURVEY.md §8(d) generator, seed 0x5EED0002 + rank) that is
+already resident in HBM, launched through the C-ABI (gasalx_align_device) on
+torch's current stream.  Multi-GPU: one process per GPU, each aligns its own
+batch (weak scaling, no data-path collective); timing is bracketed by a
+barrier + synchronize and the max over ranks is reported.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--workload sw_local|nw_tb|semi]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genomics-gpu_amd"))
+import gasal_ffi as G  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
+
+WORKLOADS = {
+    # name: (synth kind, default pairs, params, algorithmic bytes per pair, int ops per cell, label)
+    "sw_local": (2, 1_000_000, dict(algo=G.LOCAL), 332, 12,
+                 "config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp, seed 0x5EED0002"),
+    "nw_tb": (3, 100_000, dict(algo=G.GLOBAL, start_pos=G.WITH_TB), 650, 16,
+              "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
+    "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
+             "config4 shard: semi-global TARGET/TARGET, 150bp reads in 182bp windows, seed 0x5EED0004"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (default: the config's size)")
+    ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, params_kw, budget_s):
+    """The repo's CPU restatement of the GASAL2 kernels (oracle/), timed on a
+    bounded prefix of the same workload on this host's cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    op = O.make_params(**params_kw)
+    chunk = 20000
+    done_pairs, cells, t_used = 0, 0, 0.0
+    while t_used < budget_s and done_pairs < batch.n:
+        idx = np.arange(done_pairs, min(done_pairs + chunk, batch.n))
+        sub = batch.subset(idx)
+        t0 = time.perf_counter()
+        O.align(sub, op, n_threads=threads)
+        t_used += time.perf_counter() - t0
+        cells += int(np.sum(sub.q_lens.astype(np.int64) * sub.t_lens.astype(np.int64)))
+        done_pairs += len(idx)
+    return {"value": round(cells / t_used / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+            "sample": f"first {done_pairs} pairs of the rank-0 batch ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
+                      f"oracle/gasal_oracle.c OpenMP x{threads}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    kind, default_pairs, pkw, bytes_per_pair, ops_per_cell, label = WORKLOADS[args.workload]
+    n = args.pairs or default_pairs
+    seed = {2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004}[kind] + rank
+    batch = G.Batch.synth(kind, n, seed)
+    cells_per_step = int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
+    params = G.make_params(**pkw)
+
+    # inputs resident in HBM before the timed region
+    as_i32 = lambda a: torch.from_numpy(a.view(np.int32).copy()).to(dev)
+    d = {
+        "q_batch": torch.from_numpy(batch.q_data).to(dev), "t_batch": torch.from_numpy(batch.t_data).to(dev),
+        "q_offsets": as_i32(batch.q_offsets), "t_offsets": as_i32(batch.t_offsets),
+        "q_lens": as_i32(batch.q_lens), "t_lens": as_i32(batch.t_lens),
+        "aln_score": torch.empty(n, dtype=torch.int32, device=dev),
+    }
+    if pkw["algo"] != G.GLOBAL:
+        d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+        d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+    if pkw.get("start_pos") == G.WITH_TB:
+        d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
+        d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)
+    ptrs = {k: v.data_ptr() for k, v in d.items()}
+    eng = G.Engine(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
+
+    def step():
+        eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, maxq, maxt, stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        total_cells = cells_per_step * world * args.steps
+        gcups = total_cells / elapsed / 1e9
+        kern_s = kern_ms / 1e3
+        achieved = bytes_per_pair * n / kern_s / 1e9
+        valu = ops_per_cell * cells_per_step / kern_s
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %",
+            "value": round(gcups, 2),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (SURVEY.md 8(d) generator, std::mt19937_64), resident in HBM",
+            "config": {"workload": label, "pairs_per_gpu": n, "cells_per_gpu_step": cells_per_step,
+                       "plan": G.describe_plan(params, maxq, maxt), "parallelism": f"dp{world} (pairs sharded)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "bytes_per_pair": bytes_per_pair, "kernel_ms": round(kern_ms, 4)},
+            "valu_roofline": {"bound": "valu-int32", "achieved": round(valu / 1e12, 3), "peak": VALU_PEAK_OPS / 1e12,
+                              "unit": "Tops/s", "frac": round(valu / VALU_PEAK_OPS, 4), "ops_per_cell": ops_per_cell},
+            "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
+            "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(batch, pkw, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

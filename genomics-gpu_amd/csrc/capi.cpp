@@ -1,0 +1,260 @@
+// capi.cpp — extern "C" flat API (include/gasalx.h) over the engine.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "gasalx.h"
+
+struct gasalx_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    gx::Workspace ws;
+    // staging for the host-to-host entry points
+    gx::DevBuf q, t, qo, to, ql, tl, qop, top, seed;
+    gx::DevBuf o_score, o_qe, o_te, o_qs, o_ts, o_s2, o_qe2, o_te2, o_cig, o_nops, lens_max;
+    gx::DevBuf h_reads, h_ro, h_rl, h_qm, h_de, h_xi, h_al, h_haps, h_ho, h_hl, h_res;
+    void release() {
+        ws.release_all();
+        for (gx::DevBuf *b : {&q, &t, &qo, &to, &ql, &tl, &qop, &top, &seed, &o_score, &o_qe, &o_te, &o_qs, &o_ts,
+                              &o_s2, &o_qe2, &o_te2, &o_cig, &o_nops, &lens_max, &h_reads, &h_ro, &h_rl, &h_qm,
+                              &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res})
+            b->release();
+    }
+};
+
+#define CK(x)                                                                        \
+    do {                                                                             \
+        hipError_t e__ = (x);                                                        \
+        if (e__ != hipSuccess) {                                                     \
+            gx::set_error(std::string(#x) + ": " + hipGetErrorString(e__));          \
+            return e__ == hipErrorOutOfMemory ? GASALX_ENOMEM : GASALX_EDEVICE;      \
+        }                                                                            \
+    } while (0)
+
+namespace {
+
+__attribute__((unused)) uint32_t host_max(const uint32_t *a, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) m = std::max(m, a[i]);
+    return m;
+}
+
+// Read back max(q_lens), max(t_lens) from device memory (synchronises `st`).
+int device_max_lens(gasalx_engine *eng, const uint32_t *dq, const uint32_t *dt, uint32_t n, hipStream_t st,
+                    uint32_t *mq, uint32_t *mt) {
+    std::vector<uint32_t> hq(n), ht(n);
+    CK(hipMemcpyAsync(hq.data(), dq, n * 4ull, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(ht.data(), dt, n * 4ull, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    (void)eng;
+    *mq = host_max(hq.data(), n);
+    *mt = host_max(ht.data(), n);
+    return GASALX_OK;
+}
+
+template <class T>
+int stage_in(gx::DevBuf &d, const T *h, size_t count, hipStream_t st, T **dptr) {
+    *dptr = nullptr;
+    if (!h) return GASALX_OK;
+    CK(d.reserve(count * sizeof(T) + 16));
+    CK(hipMemcpyAsync(d.p, h, count * sizeof(T), hipMemcpyHostToDevice, st));
+    *dptr = d.as<T>();
+    return GASALX_OK;
+}
+
+bool valid_params(const gasalx_params *p) {
+    if (!p) return false;
+    if (p->algo < 0 || p->algo > 6) return false;
+    if (p->start_pos < 0 || p->start_pos > 2) return false;
+    if (p->head < 0 || p->head > 3 || p->tail < 0 || p->tail > 3) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gasalx_abi_version(void) { return GASALX_ABI_VERSION; }
+const char *gasalx_last_error(void) { return gx::last_error(); }
+
+int gasalx_device_count(int *count) {
+    if (!count) return GASALX_EINVAL;
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) { *count = 0; gx::set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+    *count = c;
+    return GASALX_OK;
+}
+
+int gasalx_engine_create(int device, gasalx_engine **out) {
+    if (!out) return GASALX_EINVAL;
+    *out = nullptr;
+    CK(hipSetDevice(device));
+    gasalx_engine *e = new (std::nothrow) gasalx_engine();
+    if (!e) return GASALX_ENOMEM;
+    e->device = device;
+    e->ws.device = device;
+    hipError_t he = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (he != hipSuccess) { delete e; gx::set_error(hipGetErrorString(he)); return GASALX_EDEVICE; }
+    *out = e;
+    return GASALX_OK;
+}
+
+int gasalx_engine_destroy(gasalx_engine *eng) {
+    if (!eng) return GASALX_OK;
+    (void)hipSetDevice(eng->device);
+    if (eng->stream) { (void)hipStreamSynchronize(eng->stream); (void)hipStreamDestroy(eng->stream); }
+    eng->release();
+    delete eng;
+    return GASALX_OK;
+}
+
+int gasalx_describe_plan(const gasalx_params *params, uint32_t max_q_len, uint32_t max_t_len, char *buf,
+                         uint32_t buf_len) {
+    if (!valid_params(params) || !buf || buf_len == 0) return GASALX_EINVAL;
+    gx::BatchShape s;
+    s.max_q = max_q_len; s.max_t = max_t_len;
+    gx::Plan pl = gx::make_plan(*params, s, false);
+    std::snprintf(buf, buf_len, "%s", pl.name.c_str());
+    return GASALX_OK;
+}
+
+int gasalx_align_device(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *b,
+                        const gasalx_results *out, void *stream) {
+    if (!eng || !valid_params(params) || !b || !out) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    gx::BatchShape shape;
+    shape.max_q = b->max_q_len;
+    shape.max_t = b->max_t_len;
+    if ((shape.max_q == 0 || shape.max_t == 0) && b->n_alns) {
+        int rc = device_max_lens(eng, b->q_lens, b->t_lens, b->n_alns, st, &shape.max_q, &shape.max_t);
+        if (rc) return rc;
+    }
+    return gx::align_device(eng->ws, *params, *b, *out, st, shape);
+}
+
+int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *hb,
+                      const gasalx_results *ho) {
+    if (!eng || !valid_params(params) || !hb || !ho) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    if (!hb->q_batch || !hb->t_batch || !hb->q_offsets || !hb->t_offsets || !hb->q_lens || !hb->t_lens) {
+        gx::set_error("missing batch array");
+        return GASALX_EINVAL;
+    }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    const uint32_t n = hb->n_alns;
+    gasalx_batch db = *hb;
+    int rc = 0;
+    uint8_t *p8; uint32_t *p32;
+    if ((rc = stage_in(eng->q, hb->q_batch, hb->q_bytes, st, &p8))) return rc; db.q_batch = p8;
+    if ((rc = stage_in(eng->t, hb->t_batch, hb->t_bytes, st, &p8))) return rc; db.t_batch = p8;
+    if ((rc = stage_in(eng->qo, hb->q_offsets, n, st, &p32))) return rc; db.q_offsets = p32;
+    if ((rc = stage_in(eng->to, hb->t_offsets, n, st, &p32))) return rc; db.t_offsets = p32;
+    if ((rc = stage_in(eng->ql, hb->q_lens, n, st, &p32))) return rc; db.q_lens = p32;
+    if ((rc = stage_in(eng->tl, hb->t_lens, n, st, &p32))) return rc; db.t_lens = p32;
+    if ((rc = stage_in(eng->qop, hb->q_ops, n, st, &p8))) return rc; db.q_ops = p8;
+    if ((rc = stage_in(eng->top, hb->t_ops, n, st, &p8))) return rc; db.t_ops = p8;
+    if ((rc = stage_in(eng->seed, hb->seed_scores, n, st, &p32))) return rc; db.seed_scores = p32;
+    if (!db.max_q_len) db.max_q_len = host_max(hb->q_lens, n);
+    if (!db.max_t_len) db.max_t_len = host_max(hb->t_lens, n);
+
+    // outputs: staged in with the caller's contents so fields the reference
+    // would not write come back unchanged
+    gasalx_results dout;
+    std::memset(&dout, 0, sizeof(dout));
+    int32_t *i32;
+    if ((rc = stage_in(eng->o_score, ho->aln_score, n, st, &i32))) return rc; dout.aln_score = i32;
+    if ((rc = stage_in(eng->o_qe, ho->q_end, n, st, &i32))) return rc; dout.q_end = i32;
+    if ((rc = stage_in(eng->o_te, ho->t_end, n, st, &i32))) return rc; dout.t_end = i32;
+    if ((rc = stage_in(eng->o_qs, ho->q_start, n, st, &i32))) return rc; dout.q_start = i32;
+    if ((rc = stage_in(eng->o_ts, ho->t_start, n, st, &i32))) return rc; dout.t_start = i32;
+    if ((rc = stage_in(eng->o_s2, ho->aln_score2, n, st, &i32))) return rc; dout.aln_score2 = i32;
+    if ((rc = stage_in(eng->o_qe2, ho->q_end2, n, st, &i32))) return rc; dout.q_end2 = i32;
+    if ((rc = stage_in(eng->o_te2, ho->t_end2, n, st, &i32))) return rc; dout.t_end2 = i32;
+    if ((rc = stage_in(eng->o_cig, ho->cigar, hb->q_bytes, st, &p8))) return rc; dout.cigar = p8;
+    if ((rc = stage_in(eng->o_nops, ho->n_cigar_ops, n, st, &p32))) return rc; dout.n_cigar_ops = p32;
+
+    gx::BatchShape shape;
+    shape.max_q = db.max_q_len;
+    shape.max_t = db.max_t_len;
+    rc = gx::align_device(eng->ws, *params, db, dout, st, shape);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+#define BACK(h, d, cnt)                                                                             \
+    if (h) CK(hipMemcpyAsync((void *)(h), (d), (size_t)(cnt) * sizeof(*(h)), hipMemcpyDeviceToHost, st));
+    BACK(ho->aln_score, dout.aln_score, n)
+    BACK(ho->q_end, dout.q_end, n)
+    BACK(ho->t_end, dout.t_end, n)
+    BACK(ho->q_start, dout.q_start, n)
+    BACK(ho->t_start, dout.t_start, n)
+    BACK(ho->aln_score2, dout.aln_score2, n)
+    BACK(ho->q_end2, dout.q_end2, n)
+    BACK(ho->t_end2, dout.t_end2, n)
+    BACK(ho->cigar, dout.cigar, hb->q_bytes)
+    BACK(ho->n_cigar_ops, dout.n_cigar_ops, n)
+#undef BACK
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
+int gasalx_pairhmm_device(gasalx_engine *eng, const gasalx_hmm_batch *b, float *res, void *stream) {
+    if (!eng || !b || !res) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    uint32_t mr = b->max_read_len, mh = b->max_hap_len;
+    if ((!mr || !mh) && b->n_pairs) {
+        int rc = device_max_lens(eng, b->read_lens, b->hap_lens, b->n_pairs, st, &mr, &mh);
+        if (rc) return rc;
+    }
+    return gx::pairhmm_device(eng->ws, *b, res, st, mr, mh);
+}
+
+int gasalx_pairhmm_host(gasalx_engine *eng, const gasalx_hmm_batch *hb, float *hres) {
+    if (!eng || !hb || !hres) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    const uint32_t n = hb->n_pairs;
+    gasalx_hmm_batch db = *hb;
+    int rc;
+    uint8_t *p8; uint32_t *p32; float *pf;
+    if ((rc = stage_in(eng->h_reads, hb->reads, hb->read_bytes, st, &p8))) return rc; db.reads = p8;
+    if ((rc = stage_in(eng->h_ro, hb->read_offsets, n, st, &p32))) return rc; db.read_offsets = p32;
+    if ((rc = stage_in(eng->h_rl, hb->read_lens, n, st, &p32))) return rc; db.read_lens = p32;
+    if ((rc = stage_in(eng->h_qm, hb->qm, hb->read_bytes, st, &pf))) return rc; db.qm = pf;
+    if ((rc = stage_in(eng->h_de, hb->delta, hb->read_bytes, st, &pf))) return rc; db.delta = pf;
+    if ((rc = stage_in(eng->h_xi, hb->xiksi, hb->read_bytes, st, &pf))) return rc; db.xiksi = pf;
+    if ((rc = stage_in(eng->h_al, hb->alpha, hb->read_bytes, st, &pf))) return rc; db.alpha = pf;
+    if ((rc = stage_in(eng->h_haps, hb->haps, hb->hap_bytes, st, &p8))) return rc; db.haps = p8;
+    if ((rc = stage_in(eng->h_ho, hb->hap_offsets, n, st, &p32))) return rc; db.hap_offsets = p32;
+    if ((rc = stage_in(eng->h_hl, hb->hap_lens, n, st, &p32))) return rc; db.hap_lens = p32;
+    CK(eng->h_res.reserve((size_t)n * 4 + 16));
+    uint32_t mr = hb->max_read_len ? hb->max_read_len : host_max(hb->read_lens, n);
+    uint32_t mh = hb->max_hap_len ? hb->max_hap_len : host_max(hb->hap_lens, n);
+    rc = gx::pairhmm_device(eng->ws, db, eng->h_res.as<float>(), st, mr, mh);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    CK(hipMemcpyAsync(hres, eng->h_res.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
+int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *dq, uint32_t n, float *qm,
+                          float *delta, float *xiksi, float *alpha) {
+    if (n && (!bq || !iq || !dq || !qm || !delta || !xiksi || !alpha)) return GASALX_EINVAL;
+    float ph2pr[128];
+    for (int i = 0; i < 128; i++) ph2pr[i] = powf(10.f, -((float)i) / 10.f);   // tile_1.cu:216-220
+    for (uint32_t k = 0; k < n; k++) {                                         // :415-419
+        qm[k] = ph2pr[bq[k] & 127];
+        delta[k] = ph2pr[iq[k] & 127];
+        xiksi[k] = ph2pr[dq[k] & 127];
+        alpha[k] = 1.0f - ph2pr[((int)(iq[k] & 127) + (int)(dq[k] & 127)) & 127];
+    }
+    return GASALX_OK;
+}
+
+}  // extern "C"

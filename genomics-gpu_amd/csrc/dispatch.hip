@@ -1,0 +1,313 @@
+// dispatch.hip — kernel instantiation table and the flat host dispatcher.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "engine.hpp"
+#include "generic.hpp"
+#include "pairhmm.hpp"
+#include "wavefront.hpp"
+
+namespace gx {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error() { return g_last_error.c_str(); }
+
+hipError_t DevBuf::reserve(size_t need) {
+    if (need <= bytes && p) return hipSuccess;
+    release();
+    size_t cap = std::max<size_t>(need, 256);
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) { p = nullptr; bytes = 0; return e; }
+    bytes = cap;
+    return hipSuccess;
+}
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+void Workspace::release_all() {
+    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc}) b->release();
+}
+
+// ----------------------------------------------------------------------------
+// (G lanes per pair, R rows per lane) shapes: query rows covered = G*R.
+struct Shape { int G, R; };
+static const Shape kShapes[] = {{8, 8}, {8, 12}, {8, 16}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
+
+using WfFn = void (*)(WfArgs);
+
+template <int ALGO, bool KEYS, bool TB>
+static WfFn wf_pick(int G, int R) {
+#define GX_CASE(g, r) if (G == g && R == r) return &wf_kernel<ALGO, KEYS, TB, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
+static WfFn wf_lookup(int algo, bool keys, bool tb, int G, int R) {
+    if (algo == WF_LOCAL) return tb ? wf_pick<WF_LOCAL, true, true>(G, R) : wf_pick<WF_LOCAL, true, false>(G, R);
+    if (algo == WF_GLOBAL) return tb ? wf_pick<WF_GLOBAL, false, true>(G, R) : wf_pick<WF_GLOBAL, false, false>(G, R);
+    return keys ? wf_pick<WF_SEMI, true, false>(G, R) : wf_pick<WF_SEMI, false, false>(G, R);
+}
+
+static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
+
+// Largest |value| the DP can reach, to decide whether int32 arithmetic without
+// the reference's int16 row-buffer truncation is exact.
+static bool int16_safe(const gasalx_params &p, uint32_t mq, uint32_t mt) {
+    const int64_t L = (int64_t)pad8(mq) + pad8(mt) + 16;
+    const int64_t step = (int64_t)std::max({std::abs(p.match), std::abs(p.mismatch),
+                                            p.has_n_penalty ? std::abs(p.n_penalty) : 0}) +
+                         std::abs(p.gap_open) + std::abs(p.gap_extend);
+    return std::abs((int64_t)p.gap_open) + L * step < 30000;
+}
+
+Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
+    Plan pl;
+    const uint32_t q8 = pad8(s.max_q), t8 = pad8(s.max_t);
+    const bool tb = p.start_pos == 2;
+    int wf_algo = -1;
+    bool keys = false;
+    if (p.algo == 3 /*LOCAL*/ && !p.second_best && p.start_pos != 1) { wf_algo = WF_LOCAL; keys = true; }
+    else if (p.algo == 1 /*GLOBAL*/) { wf_algo = WF_GLOBAL; }
+    else if (p.algo == 2 /*SEMI*/ && !p.second_best && p.start_pos != 1) {
+        wf_algo = WF_SEMI;
+        keys = (p.tail == 2 || p.tail == 3);
+    }
+    bool ok = wf_algo >= 0 && int16_safe(p, s.max_q, s.max_t) && t8 < 32000 && p.gap_extend >= 0;
+    if (ok) {
+        const Shape *pick = nullptr;
+        for (const Shape &sh : kShapes)
+            if ((uint32_t)(sh.G * sh.R) >= q8) { pick = &sh; break; }
+        if (!pick) ok = false;
+        else {
+            pl.G = pick->G; pl.R = pick->R;
+            pl.lds_stride = std::max<uint32_t>(t8, 8);
+            pl.lds_bytes = (size_t)kWavesPerBlock * (64 / pl.G) * pl.lds_stride;
+            if (pl.lds_bytes > 160 * 1024) ok = false;
+        }
+    }
+    if (ok) {
+        pl.kind = PLAN_WAVEFRONT;
+        pl.wf_algo = wf_algo; pl.keys = keys; pl.tb = tb && wf_algo != WF_SEMI;
+        pl.need_pack = has_ops;
+        const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";
+        pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
+                  std::to_string(pl.G) + "R" + std::to_string(pl.R);
+    } else if (p.algo == 1 || p.algo == 2 || p.algo == 3 || p.algo == 5 || p.algo == 6) {
+        pl.kind = PLAN_GENERIC;
+        pl.need_pack = true;
+        static const char *names[] = {"?", "global", "semi", "local", "?", "banded", "ksw"};
+        pl.name = std::string("generic_") + names[p.algo];
+    } else {
+        pl.kind = PLAN_NONE;
+        pl.name = "none";
+    }
+    return pl;
+}
+
+#define HIPCHK(x)                                                                        \
+    do {                                                                                 \
+        hipError_t e__ = (x);                                                            \
+        if (e__ != hipSuccess) {                                                         \
+            set_error(std::string(#x) + ": " + hipGetErrorString(e__));                  \
+            return GASALX_EDEVICE;                                                       \
+        }                                                                                \
+    } while (0)
+
+static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
+
+int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
+                 hipStream_t st, const BatchShape &shape) {
+    if (b.n_alns == 0 || b.q_bytes == 0 || b.t_bytes == 0) { set_error("empty batch"); return GASALX_EINVAL; }
+    if ((b.q_bytes & 7) || (b.t_bytes & 7)) { set_error("batch bytes not a multiple of 8"); return GASALX_EINVAL; }
+    if (!out.aln_score) { set_error("aln_score output required"); return GASALX_EINVAL; }
+    if (p.algo == 6 && !b.seed_scores) { set_error("KSW needs seed_scores"); return GASALX_EINVAL; }
+    if (shape.max_q == 0 || shape.max_t == 0) { set_error("zero-length sequence"); return GASALX_ERANGE; }
+    const bool has_ops = b.q_ops && b.t_ops;
+    Plan pl = make_plan(p, shape, has_ops);
+    const uint32_t n = b.n_alns;
+    const bool tb = p.start_pos == 2;
+
+    // TB: the device cigar buffer starts as the unpacked query batch, as in the
+    // reference where get_tb writes into unpacked_query_batch (get_tb.h:94,
+    // gasal_align.cu:281); n_cigar_ops = query_batch_lens unless get_tb runs.
+    if (tb && out.cigar && (const void *)out.cigar != (const void *)b.q_batch)
+        HIPCHK(hipMemcpyAsync(out.cigar, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
+    const bool runs_tb = tb && (p.algo == 1 || p.algo == 3) && pl.kind != PLAN_NONE;
+    if (tb && out.n_cigar_ops && !runs_tb && (const void *)out.n_cigar_ops != (const void *)b.q_lens)
+        HIPCHK(hipMemcpyAsync(out.n_cigar_ops, b.q_lens, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    if (pl.kind == PLAN_NONE) return GASALX_OK;   // UNKNOWN / MICROLOCAL: nothing launched
+
+    const uint8_t *qsrc = b.q_batch, *tsrc = b.t_batch;
+    int packed = p.is_packed ? 1 : 0;
+    if (pl.need_pack) {
+        const uint32_t qw = b.q_bytes / 8, tw = b.t_bytes / 8;
+        HIPCHK(ws.packed_q.reserve((size_t)qw * 4 + 16));
+        HIPCHK(ws.packed_t.reserve((size_t)tw * 4 + 16));
+        if (p.is_packed) {
+            HIPCHK(hipMemcpyAsync(ws.packed_q.p, b.q_batch, (size_t)qw * 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(ws.packed_t.p, b.t_batch, (size_t)tw * 4, hipMemcpyDeviceToDevice, st));
+        } else {
+            pack_kernel<<<std::min(grid_for(qw, 256), 4096), 256, 0, st>>>(b.q_batch, ws.packed_q.as<uint32_t>(), qw);
+            pack_kernel<<<std::min(grid_for(tw, 256), 4096), 256, 0, st>>>(b.t_batch, ws.packed_t.as<uint32_t>(), tw);
+        }
+        if (has_ops) {
+            revcomp_kernel<<<grid_for(n, 256), 256, 0, st>>>(ws.packed_q.as<uint32_t>(), ws.packed_t.as<uint32_t>(),
+                                                             b.q_lens, b.t_lens, b.q_offsets, b.t_offsets, b.q_ops,
+                                                             b.t_ops, n, p.n_code);
+            // with isPacked the reference's packed buffer aliases the unpacked one, so
+            // the reversed words are what the cigar D2H copy sees (ctors.cpp:64-68)
+            if (tb && out.cigar && p.is_packed)
+                HIPCHK(hipMemcpyAsync(out.cigar, ws.packed_q.p, (size_t)qw * 4, hipMemcpyDeviceToDevice, st));
+        }
+        qsrc = ws.packed_q.as<uint8_t>();
+        tsrc = ws.packed_t.as<uint8_t>();
+        packed = 1;
+    }
+
+    // traceback storage: one word per (8-column strip, padded query row)
+    const uint64_t tb_words = (uint64_t)pad8(shape.max_q) * (pad8(shape.max_t) / 8);
+    int32_t *qend = out.q_end, *tend = out.t_end;
+    if (runs_tb) {
+        HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
+        if (p.algo == 3 && (!qend || !tend)) {
+            HIPCHK(ws.ends_q.reserve((size_t)n * 4));
+            HIPCHK(ws.ends_t.reserve((size_t)n * 4));
+            if (!qend) qend = ws.ends_q.as<int32_t>();
+            if (!tend) tend = ws.ends_t.as<int32_t>();
+        }
+    }
+
+    if (pl.kind == PLAN_WAVEFRONT) {
+        WfArgs A;
+        std::memset(&A, 0, sizeof(A));
+        A.q = qsrc; A.t = tsrc;
+        A.qoff = b.q_offsets; A.toff = b.t_offsets; A.qlen = b.q_lens; A.tlen = b.t_lens;
+        A.score = out.aln_score;
+        A.qend = (p.algo == 1) ? nullptr : qend;
+        A.tend = (p.algo == 1) ? nullptr : tend;
+        A.tb = ws.tb.as<uint32_t>();
+        A.tb_pair_words = tb_words;
+        A.n = n;
+        A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
+        A.nval = p.n_code & 0xF;
+        A.has_npen = p.has_n_penalty; A.npen = p.n_penalty;
+        A.head = p.head; A.tail = p.tail;
+        A.packed = packed;
+        A.lds_stride = pl.lds_stride;
+        A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
+        WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+        if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
+        if (pl.lds_bytes > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
+        const uint32_t pairs_per_block = kWavesPerBlock * (64 / pl.G);
+        hipLaunchKernelGGL(fn, dim3(grid_for(n, pairs_per_block)), dim3(kBlock), pl.lds_bytes, st, A);
+        HIPCHK(hipGetLastError());
+    } else {
+        GenArgs A;
+        std::memset(&A, 0, sizeof(A));
+        A.qw = ws.packed_q.as<uint32_t>(); A.tw = ws.packed_t.as<uint32_t>();
+        A.qoff = b.q_offsets; A.toff = b.t_offsets; A.qlen = b.q_lens; A.tlen = b.t_lens;
+        A.seed = b.seed_scores;
+        A.score = out.aln_score; A.qend = qend; A.tend = tend; A.qstart = out.q_start; A.tstart = out.t_start;
+        A.score2 = out.aln_score2; A.qend2 = out.q_end2; A.tend2 = out.t_end2;
+        A.tb = ws.tb.as<uint32_t>(); A.tb_pair_words = tb_words;
+        const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t);
+        uint32_t maxq = p.max_query_len > 0 ? (uint32_t)p.max_query_len : std::max(q8, t8);
+        if (maxq < q8) { set_error("max_query_len smaller than a padded query"); return GASALX_ERANGE; }
+        if (p.algo == 2 && p.start_pos == 1 && maxq < t8) {
+            set_error("semi-global WITH_START needs max_query_len >= padded target length");
+            return GASALX_ERANGE;
+        }
+        A.rows_cap = std::max(maxq, q8) + 8;
+        A.maxq = (int32_t)maxq;
+        A.rev_words = maxq / 8 + 1;
+        A.n = n;
+        A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
+        A.nval = p.n_code & 0xF; A.has_npen = p.has_n_penalty; A.npen = p.n_penalty;
+        A.start_pos = p.start_pos; A.second = p.second_best; A.head = p.head; A.tail = p.tail;
+        A.kbw = p.k_band >> 3;
+        const size_t rows_elems = (size_t)A.rows_cap * n;
+        if (p.algo == 6) {
+            const size_t ke = (size_t)(shape.max_q + 8) * n;
+            HIPCHK(ws.rows_h.reserve(ke * 4));
+            HIPCHK(ws.rows_e.reserve(ke * 4));
+            gen_ksw_kernel<<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.as<int32_t>(), ws.rows_e.as<int32_t>());
+        } else {
+            HIPCHK(ws.rows_h.reserve(rows_elems * 2));
+            HIPCHK(ws.rows_e.reserve(rows_elems * 2));
+            A.rowH = ws.rows_h.as<int16_t>(); A.rowE = ws.rows_e.as<int16_t>();
+            if (p.algo == 3) gen_local_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            else if (p.algo == 2) {
+                if (p.start_pos == 1) {
+                    HIPCHK(ws.rev.reserve((size_t)2 * A.rev_words * n * 4));
+                    A.rev = ws.rev.as<uint32_t>();
+                }
+                gen_semi_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            } else if (p.algo == 5) gen_banded_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            else { set_error("global lengths beyond the wavefront shapes are not supported"); return GASALX_ERANGE; }
+        }
+        HIPCHK(hipGetLastError());
+    }
+
+    if (runs_tb && out.cigar && out.n_cigar_ops) {
+        TbArgs T;
+        T.tb = ws.tb.as<uint32_t>(); T.tb_pair_words = tb_words;
+        T.qlen = b.q_lens; T.tlen = b.t_lens; T.qoff = b.q_offsets;
+        T.score = out.aln_score; T.qend = qend; T.tend = tend;
+        T.qstart = out.q_start; T.tstart = out.t_start;
+        T.cigar = out.cigar; T.n_ops = out.n_cigar_ops; T.n = n;
+        T.a = p.match; T.b = p.mismatch; T.o = p.gap_open; T.e = p.gap_extend;
+        T.is_local = p.algo == 3;
+        tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
+        HIPCHK(hipGetLastError());
+    }
+    return GASALX_OK;
+}
+
+// ----------------------------------------------------------------------------
+using HmmFn = void (*)(HmmArgs);
+static HmmFn hmm_lookup(int G, int RR) {
+    if (RR != 8) return nullptr;
+    switch (G) {
+        case 4: return &pairhmm_kernel<4, 8>;
+        case 8: return &pairhmm_kernel<8, 8>;
+        case 16: return &pairhmm_kernel<16, 8>;
+        case 32: return &pairhmm_kernel<32, 8>;
+        case 64: return &pairhmm_kernel<64, 8>;
+        default: return nullptr;
+    }
+}
+
+int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipStream_t st, uint32_t max_r,
+                   uint32_t max_h) {
+    (void)ws;
+    if (b.n_pairs == 0) return GASALX_OK;
+    int G = 0;
+    for (int g : {4, 8, 16, 32, 64})
+        if ((uint32_t)g * 8 >= max_r) { G = g; break; }
+    if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
+    HmmArgs A;
+    A.reads = b.reads; A.roff = b.read_offsets; A.rlen = b.read_lens;
+    A.qm = b.qm; A.delta = b.delta; A.xiksi = b.xiksi; A.alpha = b.alpha;
+    A.haps = b.haps; A.hoff = b.hap_offsets; A.hlen = b.hap_lens;
+    A.result = result; A.n = b.n_pairs;
+    A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
+    const size_t lds = (size_t)4 * (64 / G) * A.lds_stride;
+    if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
+    HmmFn fn = hmm_lookup(G, 8);
+    if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(fn, dim3(grid_for(b.n_pairs, 4 * (64 / G))), dim3(256), lds, st, A);
+    HIPCHK(hipGetLastError());
+    return GASALX_OK;
+}
+
+}  // namespace gx

@@ -1,0 +1,67 @@
+// engine.hpp — host-side dispatcher of the MI355X engine.
+//
+// Replaces gasal_kernel_launcher + the KERNEL_SWITCH macro tree
+// (Non-CDP/GASAL2/src/gasal_align.cu:10-25, gasal_align.h:7-107) and the CDP
+// launch wrappers (CDP/GASAL2/src/gasal_align.cu:27-52) by one flat planner:
+// (algo, start, head, tail, secondBest, lengths) -> one kernel family + launch
+// shape, all launched from the host on one hipStream_t.  No device-side enqueue.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "gasalx.h"
+
+namespace gx {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t need);   // grow-only
+    void release();
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct Workspace {
+    int device = 0;
+    DevBuf packed_q, packed_t;      // packed words (RC / generic paths)
+    DevBuf tb;                      // traceback direction words
+    DevBuf rows_h, rows_e, rev;     // generic kernels' row buffers
+    DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
+    DevBuf misc;                    // device-side max reduction
+    void release_all();
+};
+
+enum PlanKind { PLAN_NONE = 0, PLAN_WAVEFRONT, PLAN_GENERIC };
+
+struct Plan {
+    PlanKind kind = PLAN_NONE;
+    int wf_algo = 0;        // WfAlgo
+    bool keys = false, tb = false;
+    int G = 0, R = 0;
+    uint32_t lds_stride = 0;
+    size_t lds_bytes = 0;
+    bool need_pack = false; // generic kernels / reverse-complement need packed words
+    std::string name;
+};
+
+// Host-visible summary of a batch needed for planning.
+struct BatchShape {
+    uint32_t max_q = 0, max_t = 0;
+};
+
+Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
+
+// Launch the full path for a device-resident batch on `stream`.
+// Returns GASALX_OK or an error code; sets the thread's last error message.
+int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
+                 hipStream_t stream, const BatchShape &shape);
+
+int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipStream_t stream, uint32_t max_r,
+                   uint32_t max_h);
+
+void set_error(const std::string &msg);
+const char *last_error();
+
+}  // namespace gx

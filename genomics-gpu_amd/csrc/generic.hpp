@@ -1,0 +1,541 @@
+// generic.hpp — thread-per-pair HIP kernels that walk the DP in the
+// reference's own strip-major order.  They serve the configurations whose
+// results depend on that order beyond the final maximum (local/semi-global
+// second-best, the WITH_START reverse passes), the data-dependent banded and
+// KSW kernels, and lengths beyond the wavefront kernels' register budget.
+// Row buffers live in a pair-interleaved global workspace ([row][pair]) so
+// that the 64 lanes of a wave touch consecutive words.
+//
+// Reference (Non-CDP/GASAL2/src): kernels/local_kernel_template.h:71-519,
+// kernels/semiglobal_kernel_template.h:39-388, kernels/banded.h:10-139,
+// kernels/ksw_kernel_template.h:46-199, kernels/get_tb.h:4-149,
+// kernels/pack_rc_seqs.h:13-212.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gx {
+
+struct GenArgs {
+    const uint32_t *qw, *tw;          // packed words of the whole batch
+    const uint32_t *qoff, *toff, *qlen, *tlen;
+    const uint32_t *seed;
+    int32_t *score, *qend, *tend, *qstart, *tstart;
+    int32_t *score2, *qend2, *tend2;
+    uint32_t *tb;                     // direction words (LOCAL WITH_TB), tb_pair_words per pair
+    uint64_t tb_pair_words;
+    int16_t *rowH, *rowE;             // [row][pair] scratch, rows_cap rows
+    uint32_t rows_cap;
+    uint32_t *rev;                    // [word][pair] scratch for semi-global WITH_START, 2*rev_words
+    uint32_t rev_words;
+    uint32_t n;
+    int32_t a, b, o, e, nval, has_npen, npen;
+    int32_t start_pos, second, head, tail, kbw, maxq;
+};
+
+__device__ __forceinline__ uint32_t gcode(const uint32_t *w, uint32_t pos) {
+    return (w[pos >> 3] >> (28 - ((pos & 7) << 2))) & 15u;
+}
+__device__ __forceinline__ int32_t g_sub_local(const GenArgs &A, uint32_t q, uint32_t t) {
+    int32_t v = (q == t) ? A.a : -A.b;
+    if ((int32_t)q == A.nval || (int32_t)t == A.nval) v = A.has_npen ? -A.npen : 0;
+    return v;
+}
+
+// ---------------------------------------------------------------- local ----
+__global__ __launch_bounds__(256) void gen_local_kernel(GenArgs A) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
+    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
+    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
+    const uint32_t QR = (ql + 7) >> 3, TR = (tl + 7) >> 3, Q8 = QR * 8;
+    const bool tb = A.start_pos == 2, second = A.second != 0;
+    const int32_t OE = A.o + A.e;
+#define RH(r) A.rowH[(size_t)(r) * A.n + tid]
+#define RE(r) A.rowE[(size_t)(r) * A.n + tid]
+    for (uint32_t r = 0; r < Q8; r++) { RH(r) = 0; RE(r) = 0; }
+    int32_t h[9], f[9], p[9];
+    int32_t maxHH = 0, maxY = 0, prevMax = 0, maxX = 0, max2 = 0, prev2 = 0, x2 = 0, y2 = 0;
+    for (uint32_t i = 0; i < TR; i++) {
+        for (int m = 0; m < 9; m++) h[m] = f[m] = p[m] = 0;
+        const int32_t gidx = (int32_t)(i << 3);
+        const uint32_t gpac = tw[i];
+        for (uint32_t r = 0; r < Q8; r++) {
+            const uint32_t qb = gcode(qw, r);
+            uint32_t dword = 0;
+            h[0] = RH(r);
+            int32_t e = RE(r);
+#pragma unroll
+            for (int m = 1; m <= 8; m++) {
+                const uint32_t tbase = (gpac >> (28 - 4 * (m - 1))) & 15u;
+                const int32_t tmp = p[m] + g_sub_local(A, qb, tbase);
+                const int32_t H = max(max(max(tmp, f[m]), e), 0);
+                if (tb) {
+                    const int sh = 28 - ((m - 1) << 2);
+                    const uint32_t mxo = (tmp >= p[m]) ? 0u : 1u;
+                    dword |= (H == tmp) ? (mxo << sh) : ((H == f[m]) ? (3u << sh) : (2u << sh));
+                    dword |= ((tmp - OE) > (f[m] - A.e)) ? 0u : (1u << (sh + 3));
+                    dword |= ((tmp - OE) > (e - A.e)) ? 0u : (1u << (sh + 2));
+                }
+                f[m] = max(tmp - OE, f[m] - A.e);
+                e = max(tmp - OE, e - A.e);
+                if (maxHH < H) { maxY = gidx + m - 1; maxHH = H; }
+                if (second && max2 < H && maxHH > H) { y2 = gidx + m - 1; max2 = H; }
+                h[m] = H;
+                p[m] = h[m - 1];
+            }
+            RH(r) = (int16_t)h[8];
+            RE(r) = (int16_t)e;
+            if (tb) A.tb[(uint64_t)tid * A.tb_pair_words + (uint64_t)i * Q8 + r] = dword;
+            maxX = (prevMax < maxHH) ? (int32_t)r : maxX;
+            if (second) { x2 = (prev2 < maxHH) ? (int32_t)r : x2; prev2 = max(max2, prev2); }
+            prevMax = max(maxHH, prevMax);
+        }
+    }
+    A.score[tid] = maxHH;
+    if (A.qend) A.qend[tid] = maxX;
+    if (A.tend) A.tend[tid] = maxY;
+    if (second) {
+        if (A.score2) A.score2[tid] = max2;
+        if (A.qend2) A.qend2[tid] = x2;
+        if (A.tend2) A.tend2[tid] = y2;
+    }
+    if (A.start_pos == 1) {   // WITH_START reverse pass (local :441-511)
+        const int32_t fwd = maxHH;
+        const int32_t rend_reg = min((maxX >> 3) + 1, (int32_t)QR);
+        const int32_t gend_reg = min((maxY >> 3) + 1, (int32_t)TR);
+        int32_t mH = 0, pM = 0, sx = 0, sy = 0;
+        for (uint32_t r = 0; r < Q8; r++) { RH(r) = 0; RE(r) = 0; }
+        int32_t gidx = (gend_reg << 3) + 8 - 1;
+        for (int32_t i = 0; i < gend_reg && mH < fwd; i++) {
+            for (int m = 0; m < 9; m++) h[m] = f[m] = p[m] = 0;
+            const uint32_t gpac = tw[gend_reg - 1 - i];
+            gidx -= 8;
+            int32_t ridx = (rend_reg << 3) - 1;
+            int32_t gi = 0;
+            for (int32_t j = 0; j < rend_reg && mH < fwd; j++) {
+                const uint32_t rpac = qw[rend_reg - 1 - j];
+                for (int k = 0; k <= 28 && mH < fwd; k += 4) {
+                    const uint32_t qb = (rpac >> k) & 15u;
+                    h[0] = RH(gi);
+                    int32_t e = RE(gi);
+#pragma unroll
+                    for (int m = 1; m <= 8; m++) {
+                        const uint32_t tbase = (gpac >> (4 * (m - 1))) & 15u;
+                        const int32_t tmp = p[m] + g_sub_local(A, qb, tbase);
+                        const int32_t H = max(max(max(tmp, f[m]), e), 0);
+                        f[m] = max(tmp - OE, f[m] - A.e);
+                        e = max(tmp - OE, e - A.e);
+                        if (mH < H) { sy = gidx + (m - 1); mH = H; }   // Q8
+                        h[m] = H;
+                        p[m] = h[m - 1];
+                    }
+                    RH(gi) = (int16_t)h[8];
+                    RE(gi) = (int16_t)e;
+                    sx = (pM < mH) ? ridx : sx;
+                    pM = max(mH, pM);
+                    ridx--; gi++;
+                }
+            }
+        }
+        if (A.qstart) A.qstart[tid] = sx;
+        if (A.tstart) A.tstart[tid] = sy;
+    }
+#undef RH
+#undef RE
+}
+
+// ----------------------------------------------------------- semi-global ----
+__device__ __forceinline__ void semi_rows_init(const GenArgs &A, uint32_t tid, uint32_t nrow) {
+    const bool hq = (A.head == 1 || A.head == 3);
+    for (uint32_t r = 0; r < nrow; r++) {
+        A.rowH[(size_t)r * A.n + tid] = hq ? 0 : (int16_t)((r == 0) ? 0 : -(A.o + A.e * (int32_t)r));
+        A.rowE[(size_t)r * A.n + tid] = hq ? 0 : (int16_t)-32768;
+    }
+}
+
+template <bool REV>
+__device__ void semi_pass(const GenArgs &A, uint32_t tid, const uint32_t *qw, const uint32_t *tw, uint32_t QR,
+                          uint32_t TR, uint32_t ql, uint32_t tl, int32_t i0, bool early, int32_t fwd, bool second,
+                          int32_t &maxHH, int32_t &maxY, int32_t &max2, int32_t &y2) {
+    const int32_t OE = A.o + A.e;
+    const bool ht = (A.head == 2 || A.head == 3);
+    const bool tailT = (A.tail == 2 || A.tail == 3);
+    int32_t h[9], f[9], p[9];
+    int32_t u = 1, rr = 1;
+    h[0] = 0; p[0] = 0;
+    for (int32_t i = i0; i < (int32_t)TR && (!early || maxHH < fwd); i++) {
+        const int32_t gidx = i << 3;
+        if (ht) {
+            for (int m = 0; m < 9; m++) { h[m] = 0; f[m] = -32768; p[m] = 0; }
+        } else {
+            for (int m = 1; m < 9; m++, u++, rr++) {
+                h[m] = -(A.o + A.e * (u - 1));
+                f[m] = -32768;
+                p[m] = (rr == 1) ? 0 : -(A.o + A.e * (rr - 1));
+            }
+        }
+        const uint32_t gpac = REV ? A.rev[(size_t)(A.rev_words + i) * A.n + tid] : tw[i];
+        uint32_t ridx = 0;
+        for (uint32_t j = 0; j < QR && (!early || maxHH < fwd); j++) {
+            const uint32_t rpac = REV ? A.rev[(size_t)j * A.n + tid] : qw[j];
+            for (int k = 28; k >= 0; k -= 4) {
+                const uint32_t qb = (rpac >> k) & 15u;
+                h[0] = A.rowH[(size_t)ridx * A.n + tid];
+                int32_t e = A.rowE[(size_t)ridx * A.n + tid];
+                int32_t prev = h[0] - OE;
+#pragma unroll
+                for (int m = 1; m < 9; m++) {
+                    const uint32_t tbase = (gpac >> (28 - 4 * (m - 1))) & 15u;
+                    const int32_t s = g_sub_local(A, qb, tbase);
+                    int32_t curr = h[m] - OE;
+                    f[m] = max(curr, f[m] - A.e);
+                    curr = p[m] + s;
+                    curr = max(curr, f[m]);
+                    e = max(prev, e - A.e);
+                    curr = max(curr, e);
+                    h[m] = curr;
+                    p[m] = prev + OE;
+                    prev = curr - OE;
+                }
+                A.rowH[(size_t)ridx * A.n + tid] = (int16_t)h[8];
+                A.rowE[(size_t)ridx * A.n + tid] = (int16_t)e;
+                ridx++;
+                if (tailT && ridx == ql) {
+                    for (int m = 1; m < 9; m++) {
+                        const int32_t col = gidx + m - 1;
+                        if (h[m] > maxHH && col < (int32_t)tl) { maxY = col; maxHH = h[m]; }
+                        if (second && h[m] > max2 && h[m] < maxHH && col < (int32_t)tl) { y2 = col; max2 = h[m]; }
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void gen_semi_kernel(GenArgs A) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
+    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
+    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
+    const uint32_t QR = (ql + 7) >> 3, TR = (tl + 7) >> 3;
+    const bool second = A.second != 0;
+    const bool tailQ = (A.tail == 1 || A.tail == 3);
+    const uint32_t maxq = (uint32_t)A.maxq;            // rows scanned for TAIL QUERY (:187)
+    int32_t maxHH = -32768, maxX = (int32_t)tl, maxY = (int32_t)ql;
+    int32_t max2 = -32768, x2 = (int32_t)tl, y2 = (int32_t)ql;
+    semi_rows_init(A, tid, A.rows_cap);
+    semi_pass<false>(A, tid, qw, tw, QR, TR, ql, tl, 0, false, 0, second, maxHH, maxY, max2, y2);
+    if (tailQ) {
+        for (uint32_t m = 0; m < maxq; m++) {
+            const int32_t v = A.rowH[(size_t)m * A.n + tid];
+            if (v > maxHH && m < ql) { maxX = (int32_t)m; maxHH = v; }
+            if (second && v > max2 && v < maxHH && m < tl) { x2 = (int32_t)m; max2 = v; }   // Q12
+        }
+        if (maxX != (int32_t)tl) maxY = (int32_t)ql;
+        if (second && x2 != (int32_t)tl) y2 = (int32_t)ql;
+    }
+    A.score[tid] = maxHH;
+    if (A.tend) A.tend[tid] = maxY;
+    if (A.qend) A.qend[tid] = maxX;
+    if (second) {
+        if (A.score2) A.score2[tid] = max2;
+        if (A.tend2) A.tend2[tid] = y2;
+        if (A.qend2) A.qend2[tid] = x2;
+    }
+    if (A.start_pos == 1) {   // :227-383
+        const uint32_t nw = A.rev_words;
+        for (uint32_t w = 0; w < 2 * nw; w++) A.rev[(size_t)w * A.n + tid] = 0;
+        for (int32_t i = (int32_t)ql - 1, k = 0; i >= 0; i--, k++) {
+            const uint32_t sym = gcode(qw, (uint32_t)i);
+            A.rev[(size_t)(k >> 3) * A.n + tid] |= sym << (28 - ((k & 7) << 2));
+        }
+        for (int32_t i = (int32_t)tl - 1, k = 0; i >= 0; i--, k++) {
+            const uint32_t sym = gcode(tw, (uint32_t)i);
+            A.rev[(size_t)(nw + (k >> 3)) * A.n + tid] |= sym << (28 - ((k & 7) << 2));
+        }
+        const int32_t fwd = maxHH;
+        const int32_t d = (int32_t)TR - ((maxY >> 3) + 1);
+        const int32_t gend_reg = d > 0 ? d - 1 : d;
+        int32_t rmax = -32768, ry = 0, d2 = 0, dy = 0;
+        semi_rows_init(A, tid, A.rows_cap);
+        semi_pass<true>(A, tid, qw, tw, QR, TR, ql, tl, gend_reg, true, fwd, false, rmax, ry, d2, dy);
+        if (tailQ) {
+            for (uint32_t m = 0; m < maxq; m++) {
+                const int32_t v = A.rowH[(size_t)m * A.n + tid];
+                if (v > rmax && m < ql) { maxX = (int32_t)m; rmax = v; }
+            }
+            if (maxX != (int32_t)tl) ry = (int32_t)ql;
+        }
+        if (A.tstart) A.tstart[tid] = ((int32_t)tl - 1) - ry;
+        if (A.qstart) A.qstart[tid] = ((int32_t)ql - 1) - maxX;
+    }
+}
+
+// --------------------------------------------------------------- banded ----
+__global__ __launch_bounds__(256) void gen_banded_kernel(GenArgs A) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
+    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
+    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
+    const int32_t QR = (int32_t)((ql + 7) >> 3), TR = (int32_t)((tl + 7) >> 3);
+    const int32_t OE = A.o + A.e;
+    for (int32_t r = 0; r < QR * 8; r++) { A.rowH[(size_t)r * A.n + tid] = 0; A.rowE[(size_t)r * A.n + tid] = 0; }
+    int32_t h[9], f[9], p[9];
+    int32_t maxHH = 0, prevMax = 0, maxX = 0, maxY = 0;
+    const int32_t kother = TR - (QR - A.kbw);                         // banded.h:35
+    for (int32_t i = 0; i < TR; i++) {
+        for (int m = 0; m < 9; m++) h[m] = f[m] = p[m] = 0;
+        const int32_t gidx = i << 3;
+        int32_t ridx = max(0, i - kother + 1) << 3;
+        const int32_t last_tile = min(A.kbw + i, QR);
+        const uint32_t gpac = tw[i];
+        for (int32_t j = ridx >> 3; j < last_tile; j++) {
+            const uint32_t rpac = qw[j];
+            for (int k = 28; k >= 0; k -= 4) {
+                const uint32_t qb = (rpac >> k) & 15u;
+                h[0] = A.rowH[(size_t)ridx * A.n + tid];
+                int32_t e = A.rowE[(size_t)ridx * A.n + tid];
+#pragma unroll
+                for (int m = 1; m < 9; m++) {
+                    const uint32_t tbase = (gpac >> (28 - 4 * (m - 1))) & 15u;
+                    const int32_t s = g_sub_local(A, qb, tbase);
+                    f[m] = max(h[m] - OE, f[m] - A.e);
+                    int32_t hv = max(max(p[m] + s, f[m]), 0);
+                    e = max(h[m - 1] - OE, e - A.e);
+                    hv = max(hv, e);
+                    h[m] = hv;
+                    if (maxHH < hv) { maxY = gidx + (m - 1); maxHH = hv; }
+                    p[m] = h[m - 1];
+                }
+                A.rowH[(size_t)ridx * A.n + tid] = (int16_t)h[8];
+                A.rowE[(size_t)ridx * A.n + tid] = (int16_t)e;
+                maxX = (prevMax < maxHH) ? ridx : maxX;
+                prevMax = max(maxHH, prevMax);
+                ridx++;
+            }
+        }
+    }
+    A.score[tid] = maxHH;
+    if (A.qend) A.qend[tid] = maxX;
+    if (A.tend) A.tend[tid] = maxY;
+}
+
+// ------------------------------------------------------------------ KSW ----
+// eh[] of the reference (ksw_kernel_template.h:69) = rowH (h) and rowE (e) as
+// int32 pairs in the rows scratch viewed as int32.
+__global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int32_t *ehh, int32_t *ehe) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t qlen = A.qlen[tid], tlen = A.tlen[tid];
+    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
+    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
+    const uint32_t QR = (qlen >> 3) + 1, TR = (tlen >> 3) + 1;       // Q16
+    const uint32_t h0 = A.seed ? A.seed[tid] : 0u;
+    const int o_del = A.o, o_ins = A.o, e_del = A.e, e_ins = A.e;
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+#define EH(j) ehh[(size_t)(j) * A.n + tid]
+#define EE(j) ehe[(size_t)(j) * A.n + tid]
+    for (uint32_t j = 0; j < qlen + 2; j++) { EH(j) = 0; EE(j) = 0; }
+    EH(0) = (int32_t)h0;
+    EH(1) = (h0 > (uint32_t)oe_ins) ? (int32_t)(h0 - (uint32_t)oe_ins) : 0;
+    for (int j = 2; j <= (int)qlen && EH(j - 1) > e_ins; ++j) EH(j) = EH(j - 1) - e_ins;
+    int max_ = (int32_t)h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1;
+    int beg = 0, end = (int)qlen, j = 0;
+    for (uint32_t tt = 0; tt < TR; tt++) {
+        const uint32_t gpac = tw[tt];
+        for (uint32_t tb = 0; tb < 8; tb++) {
+            const int i = (int)(tt * 8 + tb);
+            if (i >= (int)tlen) break;
+            const uint32_t gbase = (gpac >> (32 - (tb + 1) * 4)) & 0x0F;
+            int t, f = 0, h1, m = 0, mj = -1;
+            if (beg == 0) {
+                h1 = (int32_t)(h0 - (uint32_t)(o_del + e_del * (i + 1)));
+                if (h1 < 0) h1 = 0;
+            } else h1 = 0;
+            for (uint32_t qt = 0; qt < QR; qt++) {
+                const uint32_t rpac = qw[qt];
+                for (uint32_t qb = 0; qb < 8; qb++) {
+                    j = (int)(qt * 8 + qb);
+                    if (j < beg) continue;
+                    if (j >= end) break;
+                    const uint32_t rbase = (rpac >> (32 - (qb + 1) * 4)) & 0x0F;
+                    int h, M = EH(j), e = EE(j);
+                    EH(j) = h1;
+                    M = M ? M + g_sub_local(A, rbase, gbase) : 0;
+                    h = M > e ? M : e;
+                    h = h > f ? h : f;
+                    h1 = h;
+                    mj = m > h ? mj : j;
+                    m = m > h ? m : h;
+                    t = M - oe_del; t = t > 0 ? t : 0;
+                    e -= e_del; e = e > t ? e : t;
+                    EE(j) = e;
+                    t = M - oe_ins; t = t > 0 ? t : 0;
+                    f -= e_ins; f = f > t ? f : t;
+                }
+            }
+            EH(end) = h1; EE(end) = 0;
+            if (j == (int)qlen) {
+                max_ie = gscore > h1 ? max_ie : i;
+                gscore = gscore > h1 ? gscore : h1;
+            }
+            if (m == 0) break;
+            if (m > max_) { max_ = m; max_i = i; max_j = mj; }
+            for (j = beg; (j < end) && EH(j) == 0 && EE(j) == 0; ++j) ;
+            beg = j;
+            for (j = end; (j >= beg) && EH(j) == 0 && EE(j) == 0; --j) ;
+            end = j + 2 < (int)qlen ? j + 2 : (int)qlen;
+        }
+    }
+    if (gscore <= 0 || gscore <= max_ - 5) {
+        A.score[tid] = max_;
+        if (A.qend) A.qend[tid] = max_j + 1;
+        if (A.tend) A.tend[tid] = max_i + 1;
+    } else {
+        A.score[tid] = gscore;
+        if (A.qend) A.qend[tid] = (int32_t)qlen;
+        if (A.tend) A.tend[tid] = max_ie + 1;
+    }
+#undef EH
+#undef EE
+}
+
+// ------------------------------------------------------------- traceback ----
+struct TbArgs {
+    const uint32_t *tb;
+    uint64_t tb_pair_words;
+    const uint32_t *qlen, *tlen, *qoff;
+    const int32_t *score, *qend, *tend;
+    int32_t *qstart, *tstart;
+    uint8_t *cigar;
+    uint32_t *n_ops;
+    uint32_t n;
+    int32_t a, b, o, e;
+    int32_t is_local;
+};
+
+__global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
+    const uint32_t q8 = (ql + 7) & ~7u, tstrips = (tl + 7) >> 3;
+    const uint32_t *tb = A.tb + (uint64_t)tid * A.tb_pair_words;
+    const int32_t OE = A.o + A.e;
+    int i, j, total = 0, curr = 0;
+    if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
+    else { i = (int)tl; j = (int)ql; }
+    uint8_t *out = A.cigar + A.qoff[tid];
+    uint32_t prev = 0, opf = 0;
+    int n_ops = 0, off = 0, count = 0, op_select = 3, op_shift = 0;
+    while (i >= 0 && j >= 0) {
+        // get_tb.h:50-71: linear cell index over (strip, row, column)
+        const int64_t cell = ((int64_t)(i >> 3) * q8 << 3) + ((int64_t)j << 3) + (i & 7);
+        const int64_t strip = cell / (8 * (int64_t)q8);
+        const int64_t rem = cell - strip * 8 * (int64_t)q8;
+        uint32_t cell_op = 0;   // past the padded grid: 0
+        if (strip < (int64_t)tstrips)
+            cell_op = (tb[strip * q8 + (rem >> 3)] >> (28 - ((rem & 7) << 2))) & 15u;
+        const uint32_t op = (cell_op >> op_shift) & (uint32_t)op_select;
+        opf = (op == 0 || op_select == 3) ? op : (uint32_t)op_shift;
+        op_select = (op == 0 || (op == 1 && op_select == 3)) ? 3 : 1;
+        op_shift = (op == 0 || (op == 1 && op_select == 3)) ? 0 : ((op == 2 || op == 3) ? (int)op : op_shift);
+        if (count < 63 && opf == prev) {
+            count++;
+        } else {
+            if (count > 0) { out[off++] = (uint8_t)(prev | (uint32_t)(count << 2)); n_ops++; }
+            count = 1;
+        }
+        if (A.is_local) {
+            curr += ((opf == 2 || opf == 3) && prev != opf) ? -OE
+                  : ((opf == 2 || opf == 3) ? -A.e : (opf == 1 ? -A.b : A.a));
+            if (curr == total) break;
+        }
+        prev = opf;
+        i = (opf == 0 || opf == 1 || opf == 2) ? i - 1 : i;
+        j = (opf == 0 || opf == 1 || opf == 3) ? j - 1 : j;
+    }
+    out[off++] = (uint8_t)(prev | (uint32_t)(count << 2));
+    n_ops++;
+    if (!A.is_local) {
+        while (i >= 0) { const int rc = (i + 1) <= 63 ? (i + 1) : 63; out[off++] = (uint8_t)(2 | (rc << 2)); n_ops++; i -= 63; }
+        while (j >= 0) { const int rc = (j + 1) <= 63 ? (j + 1) : 63; out[off++] = (uint8_t)(3 | (rc << 2)); n_ops++; j -= 63; }
+    } else {
+        if (A.tstart) A.tstart[tid] = i;
+        if (A.qstart) A.qstart[tid] = j;
+    }
+    A.n_ops[tid] = (uint32_t)n_ops;
+}
+
+// ------------------------------------------------------- pack / revcomp ----
+// gasal_pack_kernel (pack_rc_seqs.h:13-53): 8 ASCII bytes -> one word of 4-bit
+// codes, first byte in bits 31:28.  Grid-stride over whole words.
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t *in, uint32_t *out, uint32_t n_words) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += gridDim.x * blockDim.x) {
+        const uint2 v = reinterpret_cast<const uint2 *>(in)[w];
+        uint32_t p = 0;
+        p |= (v.x & 15u) << 28; p |= ((v.x >> 8) & 15u) << 24; p |= ((v.x >> 16) & 15u) << 20; p |= ((v.x >> 24) & 15u) << 16;
+        p |= (v.y & 15u) << 12; p |= ((v.y >> 8) & 15u) << 8; p |= ((v.y >> 16) & 15u) << 4; p |= (v.y >> 24) & 15u;
+        out[w] = p;
+    }
+}
+
+__device__ __forceinline__ uint32_t shl_c(uint32_t x, uint32_t s) { return s >= 32 ? 0u : x << s; }
+__device__ __forceinline__ uint32_t shr_c(uint32_t x, uint32_t s) { return s >= 32 ? 0u : x >> s; }
+__device__ __forceinline__ uint32_t nib_rev(uint32_t x) {
+    // reverse the 8 nibbles: byte-reverse then swap nibbles within bytes
+    x = __builtin_bswap32(x);
+    return ((x & 0x0F0F0F0Fu) << 4) | ((x >> 4) & 0x0F0F0F0Fu);
+}
+
+__device__ void rc_one(uint32_t *W, uint32_t base, uint32_t len, uint8_t op, int32_t n_code) {
+    const uint32_t regs = (len + 7) >> 3;
+    if (regs == 0) return;
+    const uint32_t swaps = (regs >> 1) + (regs & 1);
+    auto RD = [&](int64_t idx) -> uint32_t { return ((int64_t)base + idx) >= 0 ? W[(int64_t)base + idx] : 0u; };
+    if (op & 1) {   // pack_rc_seqs.h:109-167 (N count is 0 for N_CODE > 15)
+        uint32_t nbr = 0;
+        const uint32_t last = W[base + regs - 1];
+        for (int jj = 0; jj < 32; jj += 4) nbr += ((int32_t)((last >> jj) & 15u) == n_code);
+        nbr <<= 2;
+        const uint32_t lowmask = shl_c(1u, nbr) - 1u;
+        for (uint32_t i = 0; i < swaps; i++) {
+            const int64_t a = (int64_t)regs - 2 - i, b = (int64_t)regs - 1 - i;
+            const uint32_t r1 = W[base + i];
+            const uint32_t r2 = shl_c(RD(a), 32 - nbr) | shr_c(RD(b), nbr);
+            const uint32_t rv1 = nib_rev(r1), rv2 = nib_rev(r2);
+            const uint32_t q1 = shl_c(rv1, nbr) | (RD(b) & lowmask);
+            const uint32_t q2 = (RD(a) & (0xFFFFFFFFu - lowmask)) | shr_c(rv1, 32 - nbr);
+            W[base + i] = rv2;
+            W[base + b] = q1;
+            if (i != swaps - 1 && (int64_t)base + a >= 0) W[base + a] = q2;
+        }
+    }
+    if (op & 2) {   // :169-205 complement A<->T (1<->4), C<->G (3<->7)
+        for (uint32_t i = 0; i < regs; i++) {
+            uint32_t rp = W[base + i], o = 0;
+            for (int k = 28; k >= 0; k -= 4) {
+                uint32_t nt = (rp >> k) & 15u;
+                nt = nt == 1 ? 4 : nt == 3 ? 7 : nt == 4 ? 1 : nt == 7 ? 3 : nt;
+                o |= nt << k;
+            }
+            W[base + i] = o;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void revcomp_kernel(uint32_t *qw, uint32_t *tw, const uint32_t *qlen,
+                                                      const uint32_t *tlen, const uint32_t *qoff,
+                                                      const uint32_t *toff, const uint8_t *qop,
+                                                      const uint8_t *top, uint32_t n, int32_t n_code) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= n) return;
+    if (qop[tid] == 0 && top[tid] == 0) return;
+    rc_one(qw, qoff[tid] >> 3, qlen[tid], qop[tid], n_code);
+    rc_one(tw, toff[tid] >> 3, tlen[tid], top[tid], n_code);
+}
+
+}  // namespace gx

@@ -1,0 +1,121 @@
+// pairhmm.hpp — PairHMM forward (fp32) as a segmented anti-diagonal wavefront.
+//
+// Reference recurrence: Non-CDP/PairHMM/inter_task/Synthetic_data/tile_1/tile_1.cu:44-177
+// (identical arithmetic in Intra-task/.../improved_warp_based.cu:91-172).
+// G lanes per pair, RR read rows per lane; haplotype bytes staged in LDS; the
+// (M, I, D) of a lane's bottom row cross to the next lane with DPP wave_shr:1.
+// Every rounding step is the reference's: products and sums are separate
+// roundings (__fmul_rn/__fadd_rn), the three FMAs are the reference's
+// __fmaf_rn sites; this file is compiled with -ffp-contract=off.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gx {
+
+struct HmmArgs {
+    const uint8_t *reads;
+    const uint32_t *roff, *rlen;
+    const float *qm, *delta, *xiksi, *alpha;
+    const uint8_t *haps;
+    const uint32_t *hoff, *hlen;
+    float *result;
+    uint32_t n;
+    uint32_t lds_stride;   // bytes per pair slot (>= max haplotype length, multiple of 4)
+};
+
+__device__ __forceinline__ float shr_lane_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+
+template <int G, int RR>
+__global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int P = 64 / G;
+    const float c0 = 1.329228e+36f, c09 = 0.9f, c01 = 0.1f;     // tile_1.cu:228-233
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lg = lane & (G - 1), slot = lane / G;
+    const uint32_t pair0 = (blockIdx.x * 4 + wave) * P;
+    const uint32_t pair = pair0 + slot;
+    const bool valid = pair < A.n;
+    uint32_t R = 0, H = 0, ro = 0, ho = 0;
+    if (valid) { R = A.rlen[pair]; H = A.hlen[pair]; ro = A.roff[pair]; ho = A.hoff[pair]; }
+
+    // stage haplotypes
+    const uint32_t stride = A.lds_stride;
+    uint8_t *wl = lds + (size_t)wave * P * stride;
+    const uint32_t words = stride >> 2;
+    for (uint32_t base = 0; base < P * words; base += 64) {
+        const uint32_t idx = base + lane;
+        const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
+        const uint32_t pH = __shfl(H, ps * G), pho = __shfl(ho, ps * G);
+        if (idx < P * words) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b)
+                if (4 * w + b < pH) v |= (uint32_t)A.haps[pho + 4 * w + b] << (8 * b);
+            reinterpret_cast<uint32_t *>(wl + ps * stride)[w] = v;
+        }
+    }
+    __syncthreads();
+    const uint8_t *hap = wl + slot * stride;
+
+    // the lane's read rows and their parameters (tile_1.cu:89-118)
+    const uint32_t r0 = lg * RR;
+    uint32_t rb[RR];
+    float qm1[RR], qm3[RR], de[RR], xi[RR], al[RR];
+    float Mk[RR], Dk[RR], MM[RR];
+#pragma unroll
+    for (int k = 0; k < RR; ++k) {
+        const uint32_t i = r0 + k;
+        const bool in = valid && i < R;
+        const float q = in ? A.qm[ro + i] : 0.f;
+        rb[k] = in ? A.reads[ro + i] : 0x100u;
+        qm1[k] = __fsub_rn(1.0f, q);                 // Qm_1 = constant[1] - Qm
+        qm3[k] = __fdiv_rn(q, 3.0f);                 // fdividef(Qm, 3) (<= 2 ulp in the reference)
+        de[k] = in ? A.delta[ro + i] : 0.f;
+        xi[k] = in ? A.xiksi[ro + i] : 0.f;
+        al[k] = in ? A.alpha[ro + i] : 0.f;
+        Mk[k] = 0.f; Dk[k] = 0.f; MM[k] = 0.f;
+    }
+    const float D0 = valid && H ? __fdiv_rn(c0, (float)H) : 0.f;      // constant[0]/(float)H
+    if (lg == 0) MM[0] = __fmul_rn(c09, D0);                           // first row's MMID (:117)
+
+    uint32_t hmax = H;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, m));
+    const uint32_t nsteps = hmax + G - 1;
+    const uint32_t last_lane = R ? (R - 1) / RR : 0;
+    const uint32_t klast = R ? (R - 1) - last_lane * RR : 0;
+    float acc = 0.f;
+    float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
+
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const int32_t j = (int32_t)s - (int32_t)lg;
+        float MU, IU, DU;
+        if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }                  // row -1: M=I=0, D=D0
+        else { MU = rM; IU = rI; DU = rD; }
+        const bool active = valid && j >= 0 && (uint32_t)j < H;
+        if (active) {
+            const uint32_t hb = hap[j];
+#pragma unroll
+            for (int k = 0; k < RR; ++k) {
+                const float MID = __fadd_rn(IU, DU);                   // :149-162
+                const float DDM = __fmul_rn(Mk[k], xi[k]);
+                const float IIMI = __fmul_rn(IU, c01);
+                const float aa = (hb == rb[k]) ? qm1[k] : qm3[k];
+                const float MIIDD = __fmul_rn(c09, MID);
+                const float Mn = __fmul_rn(aa, MM[k]);
+                const float In = __fmaf_rn(MU, de[k], IIMI);
+                const float Dn = __fmaf_rn(Dk[k], c01, DDM);
+                MM[k] = __fmaf_rn(al[k], MU, MIIDD);
+                Mk[k] = Mn; Dk[k] = Dn;
+                if (lg == last_lane && k == (int)klast) acc = __fadd_rn(acc, __fadd_rn(Mn, In));
+                MU = Mn; IU = In; DU = Dn;
+            }
+        }
+        rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+    }
+    if (valid && lg == last_lane) A.result[pair] = acc;
+}
+
+}  // namespace gx

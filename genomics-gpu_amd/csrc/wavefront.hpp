@@ -1,0 +1,371 @@
+// wavefront.hpp — segmented anti-diagonal DP kernels for gfx950 (CDNA4).
+//
+// One 64-lane wavefront aligns 64/G pairs.  Each pair owns a group of G
+// consecutive lanes; lane lg of the group owns the R consecutive query rows
+// [lg*R, lg*R+R) and holds their H/E state (and score keys, and traceback
+// words) in VGPRs.  At step s the lane computes column c = s - lg of its rows,
+// top to bottom; the bottom row's H and the F leaving it are passed to lane
+// lg+1 with one DPP wave_shr:1 each, so the group sweeps the DP matrix as an
+// anti-diagonal band.  Targets are staged once per wave in LDS (byte codes);
+// each step reads one byte per lane.  No row buffer touches memory.
+//
+// Semantics are those of the GASAL2 kernels (paths under Non-CDP/GASAL2/src):
+//   LOCAL  gasal_local_kernel          kernels/local_kernel_template.h:71-519
+//   GLOBAL gasal_global_kernel         kernels/global.h:30-303
+//   SEMI   gasal_semi_global_kernel    kernels/semiglobal_kernel_template.h:39-388
+// including the quirks listed in SURVEY.md §8 (Q1-Q7, Q9-Q11, Q15).  The
+// reference walks the matrix strip-major (8-column strips, then rows, then the
+// 8 columns); the first maximum in that order is recovered here from per-row
+// keys (score, -column) merged at the end in (strip, row, column) order (Q1).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gx {
+
+enum WfAlgo { WF_LOCAL = 0, WF_GLOBAL = 1, WF_SEMI = 2 };
+
+struct WfArgs {
+    const uint8_t *q;          // unpacked bytes, or packed words (packed != 0)
+    const uint8_t *t;
+    const uint32_t *qoff, *toff, *qlen, *tlen;
+    int32_t *score, *qend, *tend;
+    uint32_t *tb;              // direction words, tb_pair_words per pair
+    uint64_t tb_pair_words;
+    uint32_t n;
+    int32_t a, b, o, e;        // match, mismatch, gap_open, gap_extend
+    int32_t nval;              // N_CODE & 0xF
+    int32_t has_npen, npen;
+    int32_t head, tail;        // semi-global skipped head / tail (enum data_source)
+    int32_t packed;
+    uint32_t lds_stride;       // bytes of LDS per pair slot (>= max padded target + 4)
+    int32_t force_exact;       // always take the exact-N substitution path
+};
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = 64 * kWavesPerBlock;
+constexpr uint8_t kInvalidCode = 0xFF;
+
+__device__ __forceinline__ int32_t shr_lane(int32_t v) {   // lane i <- lane i-1
+    return __builtin_amdgcn_update_dpp(0, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ int32_t max3(int32_t a, int32_t b, int32_t c) {
+    return max(max(a, b), c);   // -> v_max3_i32
+}
+
+template <int G>
+__device__ __forceinline__ uint64_t group_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) {
+        uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+        uint32_t olo = __shfl_xor(lo, m), ohi = __shfl_xor(hi, m);
+        uint64_t o = ((uint64_t)ohi << 32) | olo;
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// codes of the 4 bases at padded positions [4w, 4w+4) of a sequence starting at
+// byte offset `off`, as 4 bytes (little-endian: byte k = position 4w+k)
+__device__ __forceinline__ uint32_t load4_codes(const uint8_t *base, uint32_t off, uint32_t w, int packed) {
+    if (!packed) {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(base + off + 4u * w);
+        return v & 0x0F0F0F0Fu;
+    }
+    const uint32_t word = reinterpret_cast<const uint32_t *>(base)[(off >> 3) + (w >> 1)];
+    const uint32_t half = (w & 1) ? (word & 0xFFFFu) : (word >> 16);   // 4 nibbles, first in bits 15:12
+    return ((half >> 12) & 15u) | (((half >> 8) & 15u) << 8) | (((half >> 4) & 15u) << 16) |
+           ((half & 15u) << 24);
+}
+
+template <int ALGO, bool KEYS, bool TB, int G, int R, bool EXACT>
+__device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, const uint32_t lg,
+                                        const uint32_t pair, const bool valid, const uint32_t ql,
+                                        const uint32_t tl, const uint32_t qpad, const uint32_t tpad,
+                                        const uint32_t nsteps, const uint32_t (&qc)[R], const bool (&qn)[R]) {
+    const int32_t OE = A.o + A.e;
+    const int32_t ext = A.e;
+    const int32_t NS = A.has_npen ? -A.npen : 0;          // score of an N cell (LOCAL rule)
+    const bool head_q = (A.head == 1 || A.head == 3);     // QUERY or BOTH
+    const bool head_t = (A.head == 2 || A.head == 3);     // TARGET or BOTH
+    const uint32_t r0 = lg * R;
+
+    // --- per-row state ---
+    int32_t Hk[R];     // LOCAL/GLOBAL: H(r, c-1).  SEMI: H(r, c-1) - OE
+    int32_t Ek[R];     // LOCAL/GLOBAL: E(r, c).    SEMI: E(r, c-1)
+    int32_t key[R];
+    uint32_t dw[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int32_t r = (int32_t)(r0 + k);
+        key[k] = INT32_MIN;
+        dw[k] = 0;
+        if (ALGO == WF_LOCAL) {
+            Hk[k] = 0; Ek[k] = 0;                               // local_kernel_template.h:118-120
+        } else if (ALGO == WF_GLOBAL) {
+            Hk[k] = (r == 0) ? 0 : -(A.o + A.e * r);            // global.h:57-60 (Q2)
+            Ek[k] = -32768;
+        } else {
+            const int32_t h = head_q ? 0 : ((r == 0) ? 0 : -(A.o + A.e * r));   // semiglobal :87-99
+            Hk[k] = h - OE;
+            Ek[k] = head_q ? 0 : -32768;
+        }
+    }
+    int32_t recvH = 0, prevRecvH = 0, recvF = 0;
+    if (ALGO != WF_LOCAL) {
+        // the upper lane's bottom row at column -1 (its initial H)
+        const int32_t rb = (int32_t)r0 - 1;
+        int32_t hb;
+        if (ALGO == WF_GLOBAL) hb = (rb <= 0) ? 0 : -(A.o + A.e * rb);
+        else hb = (head_q ? 0 : ((rb <= 0) ? 0 : -(A.o + A.e * rb))) - OE;
+        recvH = hb; prevRecvH = hb;
+    }
+
+    const uint32_t kq_lane = (ql - 1) / R;      // lane holding the last query row
+    const uint32_t kq = (ql - 1) - kq_lane * R;
+
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const int32_t c = (int32_t)s - (int32_t)lg;
+        // inputs arriving from the row above the lane's first row
+        int32_t diag, f;
+        if (lg == 0) {
+            if (ALGO == WF_LOCAL) { diag = 0; f = 0; }                    // p[],f[] reset per strip
+            else if (ALGO == WF_GLOBAL) {
+                diag = (c <= 0) ? 0 : -(A.o + A.e * c);                    // global.h:70
+                f = -32768;                                                // global.h:69
+            } else {
+                const int32_t hd = head_t ? 0 : ((c <= 0) ? 0 : -(A.o + A.e * c));   // :127 (p[m])
+                const int32_t hu = head_t ? 0 : -(A.o + A.e * c);                    // :125 (h[m], Q3)
+                diag = hd - OE;
+                f = max(hu - OE, -32768 - ext);
+            }
+        } else {
+            diag = prevRecvH;
+            f = recvF;
+        }
+        const bool active = valid && c >= 0 && (uint32_t)c < tpad;
+        if (active) {
+            const uint32_t tc = tcodes[c];
+            const bool tN = (int32_t)tc == A.nval;
+            int32_t Mt, Xt;
+            if (ALGO == WF_GLOBAL) {
+                Mt = (A.has_npen && tN) ? -A.npen : A.a;
+                Xt = (A.has_npen && tN) ? -A.npen : -A.b;
+            } else {
+                Mt = tN ? NS : A.a;
+                Xt = tN ? NS : -A.b;
+            }
+            const int32_t NQ = (ALGO == WF_GLOBAL) ? -A.npen : NS;
+            if (ALGO == WF_SEMI) { Mt += OE; Xt += OE; }
+            int32_t Cc = 0;
+            if (KEYS) {
+                const bool in_t = (ALGO == WF_LOCAL) ? true : ((uint32_t)c < tl);
+                Cc = (in_t ? (1 << 30) : -(1 << 30)) + (32767 - c);
+            }
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                int32_t sc = (qc[k] == tc) ? Mt : Xt;
+                if (EXACT && (ALGO != WF_GLOBAL || A.has_npen)) sc = qn[k] ? (ALGO == WF_SEMI ? NQ + OE : NQ) : sc;
+                if (ALGO == WF_SEMI) {
+                    // CORE_COMPUTE_SEMIGLOBAL (semiglobal_kernel_template.h:17-28)
+                    const int32_t E = max(Hk[k], Ek[k] - ext);          // E(r,c)
+                    const int32_t tmp = diag + sc;                       // H(r-1,c-1) + s
+                    const int32_t H = max3(tmp, f, E);
+                    Ek[k] = E;
+                    diag = Hk[k];
+                    Hk[k] = H - OE;
+                    f = max(Hk[k], f - ext);                             // F(r+1,c)
+                    if (KEYS) key[k] = max(key[k], H * 32768 + Cc);
+                } else {
+                    // CORE_LOCAL_COMPUTE / CORE_GLOBAL_COMPUTE (local :19-30, global.h:4-12)
+                    const int32_t tmp = diag + sc;
+                    int32_t H = max3(tmp, f, Ek[k]);
+                    if (ALGO == WF_LOCAL) H = max(H, 0);
+                    const int32_t toe = tmp - OE;
+                    const int32_t fm = f - ext;
+                    const int32_t em = Ek[k] - ext;
+                    if (TB) {
+                        // direction nibble (local :49-56, global.h:18-25)
+                        const uint32_t mx_ = (tmp >= diag) ? 0u : 1u;
+                        uint32_t nib = (H == tmp) ? mx_ : ((H == f) ? 3u : 2u);
+                        nib |= (toe > fm) ? 0u : 8u;
+                        nib |= (toe > em) ? 0u : 4u;
+                        dw[k] = (dw[k] << 4) | nib;
+                    }
+                    Ek[k] = max(toe, em);
+                    f = max(toe, fm);
+                    diag = Hk[k];
+                    Hk[k] = H;
+                    if (KEYS) key[k] = max(key[k], H * 32768 + Cc);
+                }
+            }
+            if (TB && ((c & 7) == 7)) {
+                uint32_t *dst = A.tb + (uint64_t)pair * A.tb_pair_words + (uint64_t)(c >> 3) * qpad + r0;
+#pragma unroll
+                for (int k = 0; k < R; k += 4) {
+                    if (r0 + k < qpad) {
+                        *reinterpret_cast<uint4 *>(dst + k) = make_uint4(dw[k], dw[k + 1], dw[k + 2], dw[k + 3]);
+                    }
+                }
+            }
+            if (ALGO == WF_GLOBAL && (uint32_t)c == tl - 1 && lg == kq_lane) {
+                int32_t h = 0;
+#pragma unroll
+                for (int k = 0; k < R; ++k) h = (k == (int)kq) ? Hk[k] : h;
+                A.score[pair] = h;                                  // global.h:98-103,299
+            }
+        }
+        // hand the bottom row to the lane below
+        prevRecvH = recvH;
+        recvH = shr_lane(Hk[R - 1]);
+        recvF = shr_lane(f);
+    }
+
+    // ---------------- results ----------------
+    if (ALGO == WF_LOCAL) {
+        // strip-major first maximum (Q1): per row (H, first column) -> order key
+        uint64_t best = 0;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint32_t r = r0 + k;
+            if (r < qpad && key[k] >= 0) {
+                const int32_t H = (key[k] >> 15) - 32768;
+                const uint32_t col = 32767u - ((uint32_t)key[k] & 0x7FFFu);
+                const uint32_t ord = (((col >> 3) * qpad + r) << 3) + (col & 7);
+                const uint64_t cand = ((uint64_t)(uint32_t)(H + (1 << 20)) << 32) | (0xFFFFFFFFu - ord);
+                best = cand > best ? cand : best;
+            }
+        }
+        best = group_max_u64<G>(best);
+        if (valid && lg == 0) {
+            int32_t H = (int32_t)(best >> 32) - (1 << 20);
+            uint32_t ord = 0xFFFFFFFFu - (uint32_t)best;
+            int32_t qe = 0, te = 0;
+            if (best == 0 || H <= 0) { H = 0; }
+            else {
+                const uint32_t col8 = ord & 7, rest = ord >> 3;
+                qe = (int32_t)(rest % qpad);
+                te = (int32_t)((rest / qpad) * 8 + col8);
+            }
+            A.score[pair] = H;                                       // local :428-430
+            if (A.qend) A.qend[pair] = qe;
+            if (A.tend) A.tend[pair] = te;
+        }
+    } else if (ALGO == WF_SEMI) {
+        const bool tail_t = (A.tail == 2 || A.tail == 3);
+        const bool tail_q = (A.tail == 1 || A.tail == 3);
+        // TAIL TARGET: row ql-1, columns < tl, first max (semiglobal :160-178)
+        uint64_t bt = 0;
+        if (KEYS && lg == kq_lane) {
+            int32_t kk = INT32_MIN;
+#pragma unroll
+            for (int k = 0; k < R; ++k) kk = (k == (int)kq) ? key[k] : kk;
+            if (kk >= 0) bt = ((uint64_t)(uint32_t)kk) | (1ull << 40);
+        }
+        // TAIL QUERY: H at the last padded column, rows < ql, first max (:185-193)
+        uint64_t bq = 0;
+        if (tail_q) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const uint32_t r = r0 + k;
+                if (r < ql) {
+                    const int32_t v = (int16_t)(Hk[k] + OE);          // short2 row buffer (Q5)
+                    const uint64_t cand = ((uint64_t)(uint32_t)(v + (1 << 20)) << 32) | (0xFFFFFFFFu - r);
+                    bq = cand > bq ? cand : bq;
+                }
+            }
+        }
+        bt = group_max_u64<G>(bt);
+        bq = group_max_u64<G>(bq);
+        if (valid && lg == 0) {
+            int32_t maxHH = -32768, maxX = (int32_t)tl, maxY = (int32_t)ql;   // :49,63-64 (Q10)
+            if (tail_t && bt != 0) {
+                const uint32_t kk = (uint32_t)bt;
+                const int32_t H = (int32_t)(kk >> 15) - 32768;
+                const int32_t col = 32767 - (int32_t)(kk & 0x7FFFu);
+                if (H > maxHH) { maxHH = H; maxY = col; }
+            }
+            if (tail_q) {
+                if (bq != 0) {
+                    const int32_t v = (int32_t)(bq >> 32) - (1 << 20);
+                    const int32_t r = (int32_t)(0xFFFFFFFFu - (uint32_t)bq);
+                    if (v > maxHH) { maxHH = v; maxX = r; }
+                }
+                if (maxX != (int32_t)tl) maxY = (int32_t)ql;               // :206-207
+            }
+            A.score[pair] = maxHH;
+            if (A.qend) A.qend[pair] = maxX;
+            if (A.tend) A.tend[pair] = maxY;
+        }
+    }
+}
+
+template <int ALGO, bool KEYS, bool TB, int G, int R>
+__global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr int P = 64 / G;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lg = lane & (G - 1);
+    const uint32_t slot = lane / G;
+    const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * P;
+    const uint32_t pair = pair0 + slot;
+    const bool valid = pair < A.n;
+
+    uint32_t ql = 0, tl = 0, qo = 0, to = 0;
+    if (valid) { ql = A.qlen[pair]; tl = A.tlen[pair]; qo = A.qoff[pair]; to = A.toff[pair]; }
+    const uint32_t qpad = (ql + 7u) & ~7u;
+    const uint32_t tpad = (tl + 7u) & ~7u;
+
+    // ---- stage the wave's P targets as byte codes in LDS ----
+    const uint32_t stride = A.lds_stride;
+    uint8_t *wlds = lds + (size_t)wave * P * stride;
+    const uint32_t words = stride >> 2;
+    for (uint32_t base = 0; base < P * words; base += 64) {   // uniform trip count: shuffles see all lanes
+        const uint32_t idx = base + lane;
+        const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
+        const uint32_t src_lane = ps * G;
+        const uint32_t ptp = __shfl(tpad, src_lane);
+        const uint32_t pto = __shfl(to, src_lane);
+        if (idx < P * words) {
+            uint32_t v = 0xFFFFFFFFu;
+            if (4u * w < ptp) v = load4_codes(A.t, pto, w, A.packed);
+            reinterpret_cast<uint32_t *>(wlds + ps * stride)[w] = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- the lane's query rows ----
+    uint32_t qc[R];
+    bool qn[R];
+    bool has_n = false;
+    const uint32_t r0 = lg * R;
+#pragma unroll
+    for (int k = 0; k < R; k += 4) {
+        uint32_t v = 0xFFFFFFFFu;
+        if (valid && r0 + k < qpad) v = load4_codes(A.q, qo, (r0 + k) >> 2, A.packed);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            qc[k + j] = (v >> (8 * j)) & 0xFFu;
+            qn[k + j] = ((int32_t)qc[k + j] == A.nval);
+            if (r0 + k + j < ql && qn[k + j]) has_n = true;
+        }
+    }
+    // steps: widest padded target of the wave + lanes of the group - 1
+    uint32_t tmaxw = tpad;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) tmaxw = max(tmaxw, (uint32_t)__shfl_xor(tmaxw, m));
+    const uint32_t nsteps = tmaxw + G - 1;
+    const uint8_t *tcodes = wlds + slot * stride;
+
+    // exact substitution only when a real query N could change a pad-free cell
+    bool exact = A.force_exact != 0;
+    if (ALGO != WF_GLOBAL || A.has_npen) exact = exact || __any(has_n);
+    if (exact)
+        wf_body<ALGO, KEYS, TB, G, R, true>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+    else
+        wf_body<ALGO, KEYS, TB, G, R, false>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+}
+
+}  // namespace gx

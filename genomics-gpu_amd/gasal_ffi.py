@@ -1,0 +1,266 @@
+"""ctypes binding of libgasal's flat C-ABI (include/gasalx.h).
+
+This is the Python side of the drop-in boundary: it mirrors the reference's
+host-side batch construction (gasal_host_batch_fill: sequences concatenated,
+each N_CODE-padded to a multiple of 8, offsets including pads, lengths without
+them — Non-CDP/GASAL2/src/host_batch.cpp:79-153, README.md:145) and calls the
+HIP engine.  There is no CPU fallback: if lib/libgasal.so is missing or no GPU
+is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgasal.so")
+
+# enum values of the reference (gasal.h:37-73)
+WITHOUT_START, WITH_START, WITH_TB = 0, 1, 2
+NONE, QUERY, TARGET, BOTH = 0, 1, 2, 3
+UNKNOWN, GLOBAL, SEMI_GLOBAL, LOCAL, MICROLOCAL, BANDED, KSW = 0, 1, 2, 3, 4, 5, 6
+N_CODE = 0x4E
+
+# exported symbols of include/gasalx.h
+EXPORTS = (
+    "gasalx_abi_version", "gasalx_last_error", "gasalx_device_count", "gasalx_engine_create",
+    "gasalx_engine_destroy", "gasalx_align_device", "gasalx_align_host", "gasalx_describe_plan",
+    "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
+    "gasalx_synth_pairs",
+)
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "match", "mismatch", "gap_open", "gap_extend", "algo", "start_pos", "second_best", "head", "tail",
+        "k_band", "is_packed", "n_code", "has_n_penalty", "n_penalty", "max_query_len")]
+
+
+class CBatch(ctypes.Structure):
+    _fields_ = [("q_batch", ctypes.c_void_p), ("q_offsets", ctypes.c_void_p), ("q_lens", ctypes.c_void_p),
+                ("t_batch", ctypes.c_void_p), ("t_offsets", ctypes.c_void_p), ("t_lens", ctypes.c_void_p),
+                ("q_bytes", ctypes.c_uint32), ("t_bytes", ctypes.c_uint32), ("n_alns", ctypes.c_uint32),
+                ("q_ops", ctypes.c_void_p), ("t_ops", ctypes.c_void_p), ("seed_scores", ctypes.c_void_p),
+                ("max_q_len", ctypes.c_uint32), ("max_t_len", ctypes.c_uint32)]
+
+
+class CResults(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "aln_score", "q_end", "t_end", "q_start", "t_start", "aln_score2", "q_end2", "t_end2", "cigar",
+        "n_cigar_ops")]
+
+
+class CHmmBatch(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_void_p), ("read_offsets", ctypes.c_void_p), ("read_lens", ctypes.c_void_p),
+                ("qm", ctypes.c_void_p), ("delta", ctypes.c_void_p), ("xiksi", ctypes.c_void_p),
+                ("alpha", ctypes.c_void_p), ("haps", ctypes.c_void_p), ("hap_offsets", ctypes.c_void_p),
+                ("hap_lens", ctypes.c_void_p), ("read_bytes", ctypes.c_uint32), ("hap_bytes", ctypes.c_uint32),
+                ("n_pairs", ctypes.c_uint32), ("max_read_len", ctypes.c_uint32), ("max_hap_len", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libgasal not built: {LIB_PATH} (run __graft_entry__.build())")
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.gasalx_last_error.restype = ctypes.c_char_p
+        for name in EXPORTS:
+            if name != "gasalx_last_error":
+                getattr(_lib, name).restype = ctypes.c_int
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().gasalx_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def make_params(algo=LOCAL, start_pos=WITHOUT_START, second_best=0, head=TARGET, tail=TARGET, match=1, mismatch=4,
+                gap_open=6, gap_extend=1, k_band=0, is_packed=0, n_code=N_CODE, n_penalty=None,
+                max_query_len=0) -> Params:
+    return Params(match, mismatch, gap_open, gap_extend, algo, start_pos, int(second_best), head, tail, k_band,
+                  is_packed, n_code, 0 if n_penalty is None else 1, 0 if n_penalty is None else n_penalty,
+                  max_query_len)
+
+
+def pad8(x):
+    return (x + 7) // 8 * 8
+
+
+@dataclass
+class Batch:
+    """A GASAL2-layout batch in host memory."""
+    q_data: np.ndarray
+    q_offsets: np.ndarray
+    q_lens: np.ndarray
+    t_data: np.ndarray
+    t_offsets: np.ndarray
+    t_lens: np.ndarray
+
+    @property
+    def n(self):
+        return len(self.q_lens)
+
+    @property
+    def q_bytes(self):
+        return len(self.q_data)
+
+    @property
+    def t_bytes(self):
+        return len(self.t_data)
+
+    @staticmethod
+    def _side(seqs):
+        lens = np.array([len(s) for s in seqs], np.uint32)
+        offs = np.zeros(len(seqs), np.uint32)
+        total = int(sum(pad8(len(s)) for s in seqs))
+        data = np.full(max(total, 8), N_CODE, np.uint8)
+        pos = 0
+        for i, s in enumerate(seqs):
+            b = s.encode() if isinstance(s, str) else bytes(s)
+            offs[i] = pos
+            data[pos:pos + len(b)] = np.frombuffer(b, np.uint8)
+            pos += pad8(len(b))
+        return data, offs, lens
+
+    @classmethod
+    def from_pairs(cls, queries, targets):
+        qd, qo, ql = cls._side(queries)
+        td, to, tl = cls._side(targets)
+        return cls(qd, qo, ql, td, to, tl)
+
+    @classmethod
+    def synth(cls, kind: int, n: int, seed: int):
+        """SURVEY.md §8(d) workloads (kind 1..4 = configs 1..4), via gasalx_synth_pairs."""
+        qb, tb = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().gasalx_synth_sizes(kind, ctypes.c_uint32(n), ctypes.byref(qb), ctypes.byref(tb)), "synth_sizes")
+        qd, td = np.zeros(qb.value, np.uint8), np.zeros(tb.value, np.uint8)
+        qo, ql, to, tl = (np.zeros(n, np.uint32) for _ in range(4))
+        _check(lib().gasalx_synth_pairs(kind, ctypes.c_uint64(seed), ctypes.c_uint32(n), _p(qd), _p(qo), _p(ql),
+                                        _p(td), _p(to), _p(tl)), "synth_pairs")
+        return cls(qd, qo, ql, td, to, tl)
+
+    def subset(self, idx):
+        """Re-pack pairs idx into a fresh batch (keeps each pair's padded bytes)."""
+        qs = [bytes(self.q_data[self.q_offsets[i]:self.q_offsets[i] + self.q_lens[i]]) for i in idx]
+        ts = [bytes(self.t_data[self.t_offsets[i]:self.t_offsets[i] + self.t_lens[i]]) for i in idx]
+        return Batch.from_pairs(qs, ts)
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+SENTINEL = -(2 ** 31) + 7
+OUT_FIELDS = ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")
+
+
+class Engine:
+    """One device workspace + stream (gasalx_engine)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().gasalx_engine_create(device, ctypes.byref(self._h)), "engine_create")
+
+    def close(self):
+        if self._h:
+            lib().gasalx_engine_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None):
+        n = batch.n
+        out = {k: np.full(n, SENTINEL, np.int32) for k in OUT_FIELDS}
+        cigar = np.zeros(batch.q_bytes, np.uint8)
+        n_ops = np.zeros(n, np.uint32)
+        qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
+        to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
+        sd = None if seed_scores is None else np.ascontiguousarray(seed_scores, np.uint32)
+        cb = CBatch(_p(batch.q_data), _p(batch.q_offsets), _p(batch.q_lens), _p(batch.t_data), _p(batch.t_offsets),
+                    _p(batch.t_lens), batch.q_bytes, batch.t_bytes, n, _p(qo), _p(to), _p(sd), 0, 0)
+        cr = CResults(*(_p(out[k]) for k in OUT_FIELDS), _p(cigar), _p(n_ops))
+        _check(lib().gasalx_align_host(self._h, ctypes.byref(params), ctypes.byref(cb), ctypes.byref(cr)),
+               "align_host")
+        out["cigar"] = cigar
+        out["n_ops"] = n_ops
+        return out
+
+    def align_device_ptrs(self, params: Params, ptrs: dict, q_bytes: int, t_bytes: int, n: int, max_q: int,
+                          max_t: int, stream: int = 0):
+        """Device-resident call: ptrs holds integer device addresses (e.g. torch tensor.data_ptr())."""
+        g = lambda k: ptrs.get(k) or None
+        cb = CBatch(g("q_batch"), g("q_offsets"), g("q_lens"), g("t_batch"), g("t_offsets"), g("t_lens"), q_bytes,
+                    t_bytes, n, g("q_ops"), g("t_ops"), g("seed_scores"), max_q, max_t)
+        cr = CResults(g("aln_score"), g("q_end"), g("t_end"), g("q_start"), g("t_start"), g("aln_score2"),
+                      g("q_end2"), g("t_end2"), g("cigar"), g("n_cigar_ops"))
+        _check(lib().gasalx_align_device(self._h, ctypes.byref(params), ctypes.byref(cb), ctypes.byref(cr),
+                                         ctypes.c_void_p(stream or None)), "align_device")
+
+    def pairhmm_host(self, reads, read_off, read_len, qm, delta, xiksi, alpha, haps, hap_off, hap_len):
+        c = lambda a, t: np.ascontiguousarray(a, t)
+        reads, haps = c(reads, np.uint8), c(haps, np.uint8)
+        arrs = [c(read_off, np.uint32), c(read_len, np.uint32), c(qm, np.float32), c(delta, np.float32),
+                c(xiksi, np.float32), c(alpha, np.float32), c(hap_off, np.uint32), c(hap_len, np.uint32)]
+        n = len(arrs[1])
+        res = np.zeros(n, np.float32)
+        hb = CHmmBatch(_p(reads), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]), _p(arrs[3]), _p(arrs[4]), _p(arrs[5]),
+                       _p(haps), _p(arrs[6]), _p(arrs[7]), len(reads), len(haps), n, 0, 0)
+        _check(lib().gasalx_pairhmm_host(self._h, ctypes.byref(hb), _p(res)), "pairhmm_host")
+        return res
+
+    def pairhmm_device_ptrs(self, ptrs: dict, read_bytes: int, hap_bytes: int, n: int, max_r: int, max_h: int,
+                            result_ptr: int, stream: int = 0):
+        g = lambda k: ptrs.get(k) or None
+        hb = CHmmBatch(g("reads"), g("read_offsets"), g("read_lens"), g("qm"), g("delta"), g("xiksi"), g("alpha"),
+                       g("haps"), g("hap_offsets"), g("hap_lens"), read_bytes, hap_bytes, n, max_r, max_h)
+        _check(lib().gasalx_pairhmm_device(self._h, ctypes.byref(hb), ctypes.c_void_p(result_ptr),
+                                           ctypes.c_void_p(stream or None)), "pairhmm_device")
+
+
+def describe_plan(params: Params, max_q: int, max_t: int) -> str:
+    buf = ctypes.create_string_buffer(128)
+    _check(lib().gasalx_describe_plan(ctypes.byref(params), max_q, max_t, buf, 128), "describe_plan")
+    return buf.value.decode()
+
+
+def pairhmm_params(bq, iq, dq):
+    n = len(bq)
+    out = [np.zeros(n, np.float32) for _ in range(4)]
+    c = lambda a: np.ascontiguousarray(a, np.uint8)
+    _check(lib().gasalx_pairhmm_params(_p(c(bq)), _p(c(iq)), _p(c(dq)), ctypes.c_uint32(n), *(_p(o) for o in out)),
+           "pairhmm_params")
+    return out
+
+
+def decode_cigar(cigar: np.ndarray, offset: int, n_ops: int) -> str:
+    """Forward CIGAR text from the reversed RLE bytes, as test_prog prints it
+    (Non-CDP/GASAL2/test_prog/test_prog.cpp:382-428)."""
+    if n_ops == 0:
+        return ""
+    ops = "MXDI"
+    b = cigar[offset:offset + n_ops]
+    last, count = int(b[-1]) & 3, int(b[-1]) >> 2
+    out = []
+    for u in range(n_ops - 2, -1, -1):
+        cur = int(b[u]) & 3
+        if cur == last:
+            count += int(b[u]) >> 2
+        else:
+            out.append(f"{count}{ops[last]}")
+            count = int(b[u]) >> 2
+        last = cur
+    out.append(f"{count}{ops[last]}")
+    return "".join(out)

@@ -1,0 +1,160 @@
+/*
+ * gasalx.h — flat C-ABI of the MI355X GASAL2-compatible engine (FFI boundary).
+ *
+ * Plain pointers and sizes only; no HIP or torch types in the signatures
+ * (streams are passed as void*, i.e. a hipStream_t).  The entry points are the
+ * ones a ctypes / cgo / JNI binding of the reference's path would bind:
+ *
+ *   gasalx_align_host    <- gasal_aln(...)   (Non-CDP/GASAL2/src/__deprecated.cpp:5,
+ *                                             the flat batch call, commented out in
+ *                                             the reference; same argument meaning,
+ *                                             plus the Parameters fields it needs)
+ *   gasalx_align_device  <- gasal_aln_async(...) (gasal_align.cu:29) without the host
+ *                           staging: inputs already resident in device memory
+ *   gasalx_pairhmm_*     <- pairHMM<<<>>> launch (Non-CDP/PairHMM/inter_task/
+ *                           Synthetic_data/tile_1/tile_1.cu:44,507-524)
+ *
+ * The reference's C++ API (gasal_header.h: gasal_init_streams, gasal_host_batch_fill,
+ * gasal_aln_async, gasal_is_aln_async_done, ...) is provided by the same library
+ * with C++ linkage.  Every call here returns 0 on success and a negative
+ * GASALX_E* code on failure (the reference exits instead, gasal.h:15-22);
+ * gasalx_last_error() gives the message of the calling thread's last failure.
+ */
+#ifndef GASALX_H
+#define GASALX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GASALX_ABI_VERSION 1
+
+enum {
+    GASALX_OK = 0,
+    GASALX_EINVAL = -1,      /* bad argument (sizes, alignment, enum value)          */
+    GASALX_ERANGE = -2,      /* sequence length / score range the engine rejects     */
+    GASALX_EDEVICE = -3,     /* HIP runtime error                                    */
+    GASALX_ENOMEM = -4,      /* device or host allocation failed                     */
+    GASALX_EUNSUPPORTED = -5 /* configuration not implemented                        */
+};
+
+/* Mirrors the Parameters fields the reference's boundary reads
+ * plus the compile-time knobs that become run-time values here. */
+typedef struct gasalx_params {
+    int32_t match;          /* gasal_subst_scores.match                              */
+    int32_t mismatch;       /* gasal_subst_scores.mismatch (penalty, positive)       */
+    int32_t gap_open;       /* gasal_subst_scores.gap_open                           */
+    int32_t gap_extend;     /* gasal_subst_scores.gap_extend                         */
+    int32_t algo;           /* enum algo_type                                        */
+    int32_t start_pos;      /* enum comp_start                                       */
+    int32_t second_best;    /* enum Bool                                             */
+    int32_t head;           /* enum data_source, semi-global skipped head            */
+    int32_t tail;           /* enum data_source, semi-global skipped tail            */
+    int32_t k_band;         /* BANDED band width in bases (kernel uses k_band >> 3)  */
+    int32_t is_packed;      /* inputs are already 4-bit packed words                 */
+    int32_t n_code;         /* reference N_CODE (0x4E for ASCII input)               */
+    int32_t has_n_penalty;  /* reference N_PENALTY defined?                          */
+    int32_t n_penalty;
+    int32_t max_query_len;  /* reference MAX_QUERY_LEN (0 = large enough for the batch) */
+} gasalx_params;
+
+/* Batch description; the pointers are device pointers for gasalx_align_device and
+ * host pointers for gasalx_align_host.  Layout as the reference's host batch:
+ * sequences concatenated, each padded with N_CODE to a multiple of 8, offsets in
+ * bytes including the pads, lengths without them (GASAL2 README.md:145). */
+typedef struct gasalx_batch {
+    const uint8_t *q_batch;
+    const uint32_t *q_offsets;
+    const uint32_t *q_lens;
+    const uint8_t *t_batch;
+    const uint32_t *t_offsets;
+    const uint32_t *t_lens;
+    uint32_t q_bytes;             /* multiple of 8 */
+    uint32_t t_bytes;             /* multiple of 8 */
+    uint32_t n_alns;
+    const uint8_t *q_ops;         /* enum operation_on_seq per pair, or NULL */
+    const uint8_t *t_ops;
+    const uint32_t *seed_scores;  /* KSW h0 per pair, or NULL */
+    uint32_t max_q_len;           /* upper bound of q_lens (0 = unknown: the engine reads   */
+    uint32_t max_t_len;           /* the lengths back, which synchronises the stream)       */
+} gasalx_batch;
+
+/* Output arrays (n_alns entries; cigar has q_bytes entries).  NULL = not wanted.
+ * Fields the reference would not write for the configuration are untouched. */
+typedef struct gasalx_results {
+    int32_t *aln_score;
+    int32_t *q_end;
+    int32_t *t_end;
+    int32_t *q_start;
+    int32_t *t_start;
+    int32_t *aln_score2;
+    int32_t *q_end2;
+    int32_t *t_end2;
+    uint8_t *cigar;          /* reversed RLE bytes at each pair's query offset     */
+    uint32_t *n_cigar_ops;
+} gasalx_results;
+
+typedef struct gasalx_engine gasalx_engine;   /* device workspace, one per thread */
+
+int gasalx_abi_version(void);
+const char *gasalx_last_error(void);
+
+int gasalx_device_count(int *count);
+int gasalx_engine_create(int device, gasalx_engine **out);
+int gasalx_engine_destroy(gasalx_engine *eng);
+
+/* Asynchronous on `stream` (a hipStream_t; NULL = the engine's own stream). */
+int gasalx_align_device(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *dev_batch,
+                        const gasalx_results *dev_out, void *stream);
+
+/* Synchronous host-to-host call (H2D, kernels, D2H). */
+int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *host_batch,
+                      const gasalx_results *host_out);
+
+/* Which kernel family the dispatcher selects for a batch (for tests/profiling):
+ * writes a short NUL-terminated name into buf. */
+int gasalx_describe_plan(const gasalx_params *params, uint32_t max_q_len, uint32_t max_t_len, char *buf,
+                         uint32_t buf_len);
+
+/* PairHMM forward.  Per read base: read byte and the four per-base parameters
+ * (qm = ph2pr[bq], delta = ph2pr[iq], xiksi = ph2pr[dq], alpha = 1 - ph2pr[(iq+dq)&127],
+ * tile_1.cu:415-419) at the read's offset; haplotype bytes at hap offsets. */
+typedef struct gasalx_hmm_batch {
+    const uint8_t *reads;
+    const uint32_t *read_offsets;
+    const uint32_t *read_lens;
+    const float *qm;
+    const float *delta;
+    const float *xiksi;
+    const float *alpha;
+    const uint8_t *haps;
+    const uint32_t *hap_offsets;
+    const uint32_t *hap_lens;
+    uint32_t read_bytes;
+    uint32_t hap_bytes;
+    uint32_t n_pairs;
+    uint32_t max_read_len;        /* upper bounds (0 = unknown, read back from the device) */
+    uint32_t max_hap_len;
+} gasalx_hmm_batch;
+
+int gasalx_pairhmm_device(gasalx_engine *eng, const gasalx_hmm_batch *dev_batch, float *dev_result, void *stream);
+int gasalx_pairhmm_host(gasalx_engine *eng, const gasalx_hmm_batch *host_batch, float *host_result);
+
+/* Host-side helper: per-base PairHMM parameters from Phred qualities
+ * (tile_1.cu:216-220 ph2pr table, :415-419). */
+int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *dq, uint32_t n, float *qm,
+                          float *delta, float *xiksi, float *alpha);
+
+/* Synthetic workloads of SURVEY.md §8(d) (benchmark/test data, std::mt19937_64).
+ * Writes a GASAL2-layout batch (N_CODE padding) into caller buffers sized by
+ * gasalx_synth_sizes.  kind: 1..4 = configs 1..4. */
+int gasalx_synth_sizes(int kind, uint32_t n_pairs, uint64_t *q_bytes, uint64_t *t_bytes);
+int gasalx_synth_pairs(int kind, uint64_t seed, uint32_t n_pairs, uint8_t *q_batch, uint32_t *q_offsets,
+                       uint32_t *q_lens, uint8_t *t_batch, uint32_t *t_offsets, uint32_t *t_lens);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

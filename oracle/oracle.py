@@ -1,0 +1,112 @@
+"""ctypes binding of the CPU oracle (oracle/build/liborc.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.  The oracle is a
+C restatement of the GASAL2 kernels (see gasal_oracle.h); parity is pinned by
+the SURVEY.md §8c known-answer vectors (tests/golden/survey_kat.json).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liborc.so")
+_lib = None
+
+# enum values of the reference (gasal.h:37-73)
+WITHOUT_START, WITH_START, WITH_TB = 0, 1, 2
+NONE, QUERY, TARGET, BOTH = 0, 1, 2, 3
+UNKNOWN, GLOBAL, SEMI_GLOBAL, LOCAL, MICROLOCAL, BANDED, KSW = 0, 1, 2, 3, 4, 5, 6
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "match", "mismatch", "gap_open", "gap_extend", "algo", "start_pos",
+        "second_best", "head", "tail", "k_band", "is_packed", "n_code",
+        "has_n_penalty", "n_penalty", "max_query_len")]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.orc_aln_batch.restype = ctypes.c_int
+        _lib.orc_pairhmm_batch.restype = ctypes.c_int
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def make_params(algo=LOCAL, start_pos=WITHOUT_START, second_best=0, head=TARGET, tail=TARGET,
+                match=1, mismatch=4, gap_open=6, gap_extend=1, k_band=0, is_packed=0,
+                n_code=0x4E, n_penalty=None, max_query_len=0) -> OrcParams:
+    return OrcParams(match, mismatch, gap_open, gap_extend, algo, start_pos, int(second_best),
+                     head, tail, k_band, is_packed, n_code,
+                     0 if n_penalty is None else 1, 0 if n_penalty is None else n_penalty,
+                     max_query_len)
+
+
+SENTINEL = -(2 ** 31) + 7
+
+
+def align(batch, params: OrcParams, q_ops=None, t_ops=None, seed_scores=None, n_threads=0):
+    """Run the oracle on a Batch (see tests/batch.py).  Returns dict of arrays;
+    fields the reference would not write stay at SENTINEL."""
+    n = batch.n
+    out = {k: np.full(n, SENTINEL, np.int32) for k in
+           ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")}
+    cigar = np.zeros(batch.q_bytes, np.uint8)
+    n_ops = np.zeros(n, np.uint32)
+    qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
+    to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
+    sd = None if seed_scores is None else np.ascontiguousarray(seed_scores, np.uint32)
+    rc = lib().orc_aln_batch(
+        ctypes.byref(params),
+        _ptr(batch.q_data), _ptr(batch.q_offsets), _ptr(batch.q_lens),
+        _ptr(batch.t_data), _ptr(batch.t_offsets), _ptr(batch.t_lens),
+        ctypes.c_uint32(batch.q_bytes), ctypes.c_uint32(batch.t_bytes), ctypes.c_uint32(n),
+        _ptr(qo), _ptr(to), _ptr(sd),
+        _ptr(out["score"]), _ptr(out["q_end"]), _ptr(out["t_end"]),
+        _ptr(out["q_start"]), _ptr(out["t_start"]),
+        _ptr(out["score2"]), _ptr(out["q_end2"]), _ptr(out["t_end2"]),
+        _ptr(cigar), _ptr(n_ops), ctypes.c_int(n_threads))
+    if rc != 0:
+        raise ValueError(f"orc_aln_batch failed: {rc}")
+    out["cigar"] = cigar
+    out["n_ops"] = n_ops
+    return out
+
+
+def pairhmm_params(bq, iq, dq):
+    n = len(bq)
+    qm, de, xi, al = (np.zeros(n, np.float32) for _ in range(4))
+    lib().orc_pairhmm_params(_ptr(np.ascontiguousarray(bq, np.uint8)),
+                             _ptr(np.ascontiguousarray(iq, np.uint8)),
+                             _ptr(np.ascontiguousarray(dq, np.uint8)), ctypes.c_uint32(n),
+                             _ptr(qm), _ptr(de), _ptr(xi), _ptr(al))
+    return qm, de, xi, al
+
+
+def pairhmm(reads, read_off, read_len, qm, delta, xiksi, alpha, haps, hap_off, hap_len, n_threads=0):
+    n = len(read_len)
+    res = np.zeros(n, np.float32)
+    c = lambda a, t: np.ascontiguousarray(a, t)
+    lib().orc_pairhmm_batch(ctypes.c_uint32(n), _ptr(c(reads, np.uint8)), _ptr(c(read_off, np.uint32)),
+                            _ptr(c(read_len, np.uint32)), _ptr(c(qm, np.float32)), _ptr(c(delta, np.float32)),
+                            _ptr(c(xiksi, np.float32)), _ptr(c(alpha, np.float32)), _ptr(c(haps, np.uint8)),
+                            _ptr(c(hap_off, np.uint32)), _ptr(c(hap_len, np.uint32)), _ptr(res),
+                            ctypes.c_int(n_threads))
+    return res

@@ -1,0 +1,257 @@
+"""GPU parity: the HIP engine (through the C-ABI, gasal_ffi) against the CPU
+oracle on identical inputs.  Integer outputs must match bit-exactly; PairHMM
+within 1e-5 relative (BASELINE.json north_star)."""
+import os
+
+import numpy as np
+import pytest
+
+import gasal_ffi as G
+import helpers
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _build():
+    O.build()
+
+
+def _params_pair(**kw):
+    return G.make_params(**kw), O.make_params(**kw)
+
+
+def check(engine, batch, q_ops=None, t_ops=None, seed=None, cigar=False, **kw):
+    gp, op = _params_pair(**kw)
+    g = engine.align_host(batch, gp, q_ops=q_ops, t_ops=t_ops, seed_scores=seed)
+    o = O.align(batch, op, q_ops=q_ops, t_ops=t_ops, seed_scores=seed)
+    for f in FIELDS:
+        bad = np.nonzero(g[f] != o[f])[0]
+        assert bad.size == 0, (f"{f}: {bad.size}/{batch.n} mismatches; first #{bad[0]}: gpu={g[f][bad[0]]} "
+                               f"oracle={o[f][bad[0]]} q={batch.q_lens[bad[0]]} t={batch.t_lens[bad[0]]} kw={kw}")
+    if cigar:
+        assert np.array_equal(g["n_ops"], o["n_ops"]), "n_cigar_ops differ"
+        assert np.array_equal(g["cigar"], o["cigar"]), "cigar bytes differ"
+    return g, o
+
+
+def rand_batch(seed, n, qmin, qmax, tmin, tmax, alphabet=b"ACGT", related=0.7):
+    rng = np.random.default_rng(seed)
+    qs, ts = helpers.random_pairs(rng, n, qmin, qmax, tmin, tmax, related=related, alphabet=alphabet)
+    return G.Batch.from_pairs(qs, ts)
+
+
+# ------------------------------------------------------------------ KATs ----
+def test_kat_through_gpu(engine):
+    kat = helpers.kat()
+    b = G.Batch.from_pairs([p["q"] for p in kat["pairs"]], [p["t"] for p in kat["pairs"]])
+    gp = G.make_params(algo=G.LOCAL)
+    r = engine.align_host(b, gp)
+    for i, p in enumerate(kat["pairs"]):
+        assert (r["score"][i], r["q_end"][i], r["t_end"][i]) == (p["local"]["score"], p["local"]["q_end"],
+                                                                 p["local"]["t_end"])
+    r = engine.align_host(b, G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB))
+    for i, p in enumerate(kat["pairs"]):
+        e = p["global_tb"]
+        assert r["score"][i] == e["score"] and r["n_ops"][i] == e["n_ops"]
+        off = int(b.q_offsets[i])
+        assert list(r["cigar"][off:off + e["n_ops"]]) == e["bytes_rev"]
+    r = engine.align_host(b, G.make_params(algo=G.SEMI_GLOBAL))
+    for i, p in enumerate(kat["pairs"]):
+        e = p["semi_tt"]
+        assert (r["score"][i], r["q_end"][i], r["t_end"][i]) == (e["score"], e["q_end"], e["t_end"])
+
+
+# ----------------------------------------------------------------- local ----
+@pytest.mark.parametrize("qr,tr", [((1, 40), (1, 40)), ((60, 64), (60, 64)), ((140, 160), (140, 160)),
+                                   ((150, 150), (150, 150)), ((200, 320), (150, 400)), ((600, 1200), (500, 900))])
+def test_local_random(engine, qr, tr):
+    b = rand_batch(hash((qr, tr)) & 0xFFFF, 700, *qr, *tr)
+    check(engine, b, algo=G.LOCAL)
+
+
+def test_local_with_n_bases(engine):
+    b = rand_batch(11, 800, 20, 150, 20, 150, alphabet=b"ACGTN")
+    check(engine, b, algo=G.LOCAL)
+
+
+def test_local_other_iupac_and_lowercase(engine):
+    b = rand_batch(12, 500, 30, 120, 30, 120, alphabet=b"ACGTacgtRYKMSWN")
+    check(engine, b, algo=G.LOCAL)
+
+
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2), (5, 4, 10, 1), (1, 1, 0, 1), (3, 6, 0, 0)])
+def test_local_scores(engine, scores):
+    a, bb, o, e = scores
+    b = rand_batch(13 + a, 500, 50, 160, 50, 160)
+    check(engine, b, algo=G.LOCAL, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+
+
+def test_local_sample_fasta(engine):
+    q, t, _, _ = helpers.read_fasta_pairs(limit=3000)
+    check(engine, G.Batch.from_pairs(q, t), algo=G.LOCAL)
+
+
+def test_local_traceback(engine):
+    q, t, _, _ = helpers.read_fasta_pairs(limit=1500)
+    check(engine, G.Batch.from_pairs(q, t), algo=G.LOCAL, start_pos=G.WITH_TB, cigar=True)
+    check(engine, rand_batch(21, 500, 10, 100, 10, 100), algo=G.LOCAL, start_pos=G.WITH_TB, cigar=True)
+
+
+def test_local_with_start(engine):
+    q, t, _, _ = helpers.read_fasta_pairs(limit=800)
+    check(engine, G.Batch.from_pairs(q, t), algo=G.LOCAL, start_pos=G.WITH_START)
+
+
+def test_local_second_best(engine):
+    check(engine, rand_batch(22, 600, 30, 150, 30, 200), algo=G.LOCAL, second_best=1)
+
+
+# ---------------------------------------------------------------- global ----
+@pytest.mark.parametrize("qr,tr", [((1, 30), (1, 30)), ((290, 310), (290, 310)), ((300, 300), (300, 300)),
+                                   ((100, 1000), (100, 1000))])
+def test_global_random(engine, qr, tr):
+    b = rand_batch(31 + qr[0], 600, *qr, *tr)
+    check(engine, b, algo=G.GLOBAL)
+
+
+def test_global_traceback_len_not_mult8(engine):
+    rng = np.random.default_rng(32)
+    qs, ts = [], []
+    while len(qs) < 800:
+        q, t = helpers.random_pairs(rng, 1, 20, 310, 20, 310)
+        if len(q[0]) % 8 and len(t[0]) % 8:
+            qs += q; ts += t
+    check(engine, G.Batch.from_pairs(qs, ts), algo=G.GLOBAL, start_pos=G.WITH_TB, cigar=True)
+
+
+def test_global_traceback_any_len(engine):
+    # lengths = 0 mod 8 hit SURVEY Q9 (a read past the padded grid, defined as 0 here and in the oracle)
+    check(engine, rand_batch(33, 600, 8, 64, 8, 64), algo=G.GLOBAL, start_pos=G.WITH_TB, cigar=True)
+
+
+# ----------------------------------------------------------- semi-global ----
+@pytest.mark.parametrize("head", [G.NONE, G.QUERY, G.TARGET, G.BOTH])
+@pytest.mark.parametrize("tail", [G.NONE, G.QUERY, G.TARGET, G.BOTH])
+def test_semiglobal_head_tail(engine, head, tail):
+    b = rand_batch(40 + head * 4 + tail, 400, 20, 160, 20, 200)
+    check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail)
+
+
+@pytest.mark.parametrize("head,tail", [(G.TARGET, G.TARGET), (G.BOTH, G.BOTH), (G.NONE, G.QUERY)])
+def test_semiglobal_second_best(engine, head, tail):
+    b = rand_batch(50 + head, 300, 20, 150, 20, 150)
+    check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, second_best=1, max_query_len=160)
+
+
+@pytest.mark.parametrize("head,tail", [(G.TARGET, G.TARGET), (G.NONE, G.NONE), (G.QUERY, G.BOTH)])
+def test_semiglobal_with_start(engine, head, tail):
+    b = rand_batch(60 + head, 300, 20, 150, 20, 150)
+    check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, start_pos=G.WITH_START, max_query_len=160)
+
+
+def test_semiglobal_reads_in_windows(engine):
+    b = G.Batch.synth(4, 2000, 0x5EED0004)
+    check(engine, b, algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET)
+
+
+# --------------------------------------------------------- banded / KSW ----
+@pytest.mark.parametrize("k_band", [8, 16, 48])
+def test_banded(engine, k_band):
+    check(engine, rand_batch(70 + k_band, 400, 30, 150, 30, 200), algo=G.BANDED, k_band=k_band)
+
+
+def test_ksw(engine):
+    b = rand_batch(80, 500, 10, 150, 10, 150)
+    seed = np.random.default_rng(81).integers(0, 60, b.n).astype(np.uint32)
+    check(engine, b, seed=seed, algo=G.KSW)
+
+
+# ------------------------------------------------ reverse / complement ----
+@pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL, G.SEMI_GLOBAL])
+def test_reverse_complement_ops(engine, algo):
+    b = rand_batch(90 + algo, 500, 10, 150, 10, 150)
+    rng = np.random.default_rng(91)
+    qo = rng.integers(0, 4, b.n).astype(np.uint8)
+    to = rng.integers(0, 4, b.n).astype(np.uint8)
+    check(engine, b, q_ops=qo, t_ops=to, algo=algo)
+
+
+def test_packed_input(engine):
+    b = rand_batch(95, 400, 10, 150, 10, 150)
+    pq = np.zeros(b.q_bytes // 8, np.uint32)
+    pt = np.zeros(b.t_bytes // 8, np.uint32)
+    O.lib().orc_pack(O._ptr(b.q_data), np.uint32(b.q_bytes), O._ptr(pq))
+    O.lib().orc_pack(O._ptr(b.t_data), np.uint32(b.t_bytes), O._ptr(pt))
+    bp = G.Batch(pq.view(np.uint8).copy(), b.q_offsets, b.q_lens, pt.view(np.uint8).copy(), b.t_offsets, b.t_lens)
+    # the packed buffer is bytes/2 long; lengths/offsets keep the unpacked units (offsets >> 3 = word index)
+    bp.q_data = np.concatenate([bp.q_data, np.zeros(b.q_bytes - len(bp.q_data), np.uint8)])
+    bp.t_data = np.concatenate([bp.t_data, np.zeros(b.t_bytes - len(bp.t_data), np.uint8)])
+    g1 = check(engine, bp, algo=G.LOCAL, is_packed=1)[0]
+    g0 = engine.align_host(b, G.make_params(algo=G.LOCAL))
+    assert np.array_equal(g0["score"], g1["score"])
+
+
+# ----------------------------------------------------- full-size configs ----
+def test_plan_is_wavefront_for_bench_configs():
+    assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150).startswith("wavefront_local")
+    assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300).startswith("wavefront_global_tb")
+    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL), 150, 182).startswith("wavefront_semi")
+
+
+def test_config2_sample_exact(engine):
+    b = G.Batch.synth(2, 40000, 0x5EED0002)
+    check(engine, b, algo=G.LOCAL)
+
+
+def test_config3_sample_exact(engine):
+    b = G.Batch.synth(3, 4000, 0x5EED0003)
+    check(engine, b, algo=G.GLOBAL, start_pos=G.WITH_TB, cigar=True)
+
+
+# --------------------------------------------------------------- PairHMM ----
+def _hmm_batch(pairs):
+    reads = b"".join(p["read"].encode() for p in pairs)
+    haps = b"".join(p["hap"].encode() for p in pairs)
+    rl = np.array([len(p["read"]) for p in pairs], np.uint32)
+    hl = np.array([len(p["hap"]) for p in pairs], np.uint32)
+    ro = np.concatenate([[0], np.cumsum(rl)[:-1]]).astype(np.uint32)
+    ho = np.concatenate([[0], np.cumsum(hl)[:-1]]).astype(np.uint32)
+    bq = np.concatenate([p["bq"] for p in pairs]).astype(np.uint8)
+    iq = np.concatenate([p["iq"] for p in pairs]).astype(np.uint8)
+    dq = np.concatenate([p["dq"] for p in pairs]).astype(np.uint8)
+    qm, de, xi, al = O.pairhmm_params(bq, iq, dq)
+    return (np.frombuffer(reads, np.uint8), ro, rl, qm, de, xi, al, np.frombuffer(haps, np.uint8), ho, hl)
+
+
+def test_pairhmm_reference_datasets(engine):
+    d = os.path.join(helpers.GOLDEN, "pairhmm_dataset")
+    pairs = [helpers.read_pairhmm_dataset(os.path.join(d, f))[0] for f in sorted(os.listdir(d))]
+    args = _hmm_batch(pairs)
+    g = engine.pairhmm_host(*args)
+    o = O.pairhmm(*args)
+    np.testing.assert_allclose(g, o, rtol=1e-5)
+    kat = helpers.kat()["pairhmm_32_32"]
+    i = sorted(os.listdir(d)).index(kat["file"])
+    assert abs(g[i] - kat["result"]) / kat["result"] < 1e-5
+
+
+def test_pairhmm_random_long(engine):
+    rng = np.random.default_rng(5)
+    pairs = []
+    for _ in range(300):
+        H = int(rng.integers(50, 520))
+        R = int(rng.integers(20, min(H, 300)))
+        hap = helpers.random_seq(rng, H).decode()
+        st = int(rng.integers(0, H - R + 1))
+        read = bytearray(hap[st:st + R].encode())
+        for i in range(R):
+            if rng.random() < 0.02:
+                read[i] = b"ACGT"[int(rng.integers(0, 4))]
+        pairs.append(dict(read=read.decode(), hap=hap, bq=rng.integers(10, 41, R), iq=np.full(R, 45),
+                          dq=np.full(R, 45)))
+    args = _hmm_batch(pairs)
+    np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
