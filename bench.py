@@ -108,7 +108,8 @@ def main():
         d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)
     ptrs = {k: v.data_ptr() for k, v in d.items()}
     eng = G.Engine(local_rank)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)      # a real (non-null) stream: kernels and timing events share it
+    torch.cuda.set_stream(stream)
     maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
 
     def step():

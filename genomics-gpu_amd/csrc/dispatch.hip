@@ -10,6 +10,7 @@
 #include "generic.hpp"
 #include "pairhmm.hpp"
 #include "wavefront.hpp"
+#include "wavefront16.hpp"
 
 namespace gx {
 
@@ -57,7 +58,25 @@ static WfFn wf_lookup(int algo, bool keys, bool tb, int G, int R) {
     return keys ? wf_pick<WF_SEMI, true, false>(G, R) : wf_pick<WF_SEMI, false, false>(G, R);
 }
 
+static WfFn wf16_lookup(int G, int R) {
+#define GX_CASE(g, r) if (G == g && R == r) return &wf16_local_kernel<g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
 static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
+
+// The packed kernel is exact when every DP value fits its 16-bit key field.
+static bool packed16_ok(const gasalx_params &p, uint32_t mq, uint32_t mt) {
+    if (p.algo != 3 || p.second_best || p.start_pos != 0) return false;
+    if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
+    if (p.has_n_penalty && p.n_penalty < 0) return false;
+    if (p.gap_open + p.gap_extend > 16000 || p.mismatch > 16000) return false;
+    if ((int64_t)p.match * std::min(mq, mt) > 255) return false;
+    return pad8(mt) <= 256;
+}
 
 // Largest |value| the DP can reach, to decide whether int32 arithmetic without
 // the reference's int16 row-buffer truncation is exact.
@@ -98,9 +117,15 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         pl.kind = PLAN_WAVEFRONT;
         pl.wf_algo = wf_algo; pl.keys = keys; pl.tb = tb && wf_algo != WF_SEMI;
         pl.need_pack = has_ops;
+        pl.packed16 = packed16_ok(p, s.max_q, s.max_t);
+        if (pl.packed16) {
+            const uint32_t words = (t8 + 2 * pl.G + 4 + 3) & ~3u;   // odd-step tail + prefetch
+            pl.lds_stride = words * 4;
+            pl.lds_bytes = (size_t)kWavesPerBlock * (64 / pl.G) * pl.lds_stride;
+        }
         const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";
-        pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
-                  std::to_string(pl.G) + "R" + std::to_string(pl.R);
+        pl.name = std::string(pl.packed16 ? "wavefront16_" : "wavefront_") + an + (pl.tb ? "_tb" : "") +
+                  (keys && !pl.packed16 ? "_keys" : "") + "_G" + std::to_string(pl.G) + "R" + std::to_string(pl.R);
     } else if (p.algo == 1 || p.algo == 2 || p.algo == 3 || p.algo == 5 || p.algo == 6) {
         pl.kind = PLAN_GENERIC;
         pl.need_pack = true;
@@ -204,11 +229,12 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.packed = packed;
         A.lds_stride = pl.lds_stride;
         A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
-        WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+        A.one = 0x00010001u;
+        WfFn fn = pl.packed16 ? wf16_lookup(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
         if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
-        const uint32_t pairs_per_block = kWavesPerBlock * (64 / pl.G);
+        const uint32_t pairs_per_block = kWavesPerBlock * (64 / pl.G) * (pl.packed16 ? 2 : 1);
         hipLaunchKernelGGL(fn, dim3(grid_for(n, pairs_per_block)), dim3(kBlock), pl.lds_bytes, st, A);
         HIPCHK(hipGetLastError());
     } else {

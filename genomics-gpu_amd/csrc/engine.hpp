@@ -39,6 +39,7 @@ struct Plan {
     PlanKind kind = PLAN_NONE;
     int wf_algo = 0;        // WfAlgo
     bool keys = false, tb = false;
+    bool packed16 = false;  // two pairs per lane in int16 halves (wavefront16.hpp)
     int G = 0, R = 0;
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;

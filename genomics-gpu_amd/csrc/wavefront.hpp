@@ -40,6 +40,7 @@ struct WfArgs {
     int32_t packed;
     uint32_t lds_stride;       // bytes of LDS per pair slot (>= max padded target + 4)
     int32_t force_exact;       // always take the exact-N substitution path
+    uint32_t one;              // 0x00010001 (opaque to the compiler, see wavefront16.hpp)
 };
 
 constexpr int kWavesPerBlock = 4;
