@@ -176,7 +176,8 @@ __device__ void semi_pass(const GenArgs &A, uint32_t tid, const uint32_t *qw, co
                 p[m] = (rr == 1) ? 0 : -(A.o + A.e * (rr - 1));
             }
         }
-        const uint32_t gpac = REV ? A.rev[(size_t)(A.rev_words + i) * A.n + tid] : tw[i];
+        // negative strips (gend_reg < 0) read zero words, as in the oracle
+        const uint32_t gpac = i < 0 ? 0u : (REV ? A.rev[(size_t)(A.rev_words + i) * A.n + tid] : tw[i]);
         uint32_t ridx = 0;
         for (uint32_t j = 0; j < QR && (!early || maxHH < fwd); j++) {
             const uint32_t rpac = REV ? A.rev[(size_t)j * A.n + tid] : qw[j];

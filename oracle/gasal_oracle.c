@@ -289,7 +289,10 @@ static void semi_pass(const scores_t *sc, int head, int tail, int second,
                 p[m] = (rr == 1) ? 0 : -(sc->o + sc->e * (rr - 1));
             }
         }
-        const uint32_t gpac = twords[i];
+        /* the WITH_START pass can start at a negative strip (gend_reg < 0 when the
+         * end row lies past the target, :273); the reference then reads its
+         * reverse_target_batch[] out of bounds.  Defined here as zero words. */
+        const uint32_t gpac = i >= 0 ? twords[i] : 0u;
         uint32_t ridx = 0;
         for (uint32_t j = 0; j < QR && (!early_stop || *maxHH < fwd); j++) {
             const uint32_t rpac = qwords[j];

@@ -201,8 +201,9 @@ def test_packed_input(engine):
     b = rand_batch(95, 400, 10, 150, 10, 150)
     pq = np.zeros(b.q_bytes // 8, np.uint32)
     pt = np.zeros(b.t_bytes // 8, np.uint32)
-    O.lib().orc_pack(O._ptr(b.q_data), np.uint32(b.q_bytes), O._ptr(pq))
-    O.lib().orc_pack(O._ptr(b.t_data), np.uint32(b.t_bytes), O._ptr(pt))
+    import ctypes
+    O.lib().orc_pack(O._ptr(b.q_data), ctypes.c_uint32(b.q_bytes), O._ptr(pq))
+    O.lib().orc_pack(O._ptr(b.t_data), ctypes.c_uint32(b.t_bytes), O._ptr(pt))
     bp = G.Batch(pq.view(np.uint8).copy(), b.q_offsets, b.q_lens, pt.view(np.uint8).copy(), b.t_offsets, b.t_lens)
     # the packed buffer is bytes/2 long; lengths/offsets keep the unpacked units (offsets >> 3 = word index)
     bp.q_data = np.concatenate([bp.q_data, np.zeros(b.q_bytes - len(bp.q_data), np.uint8)])
