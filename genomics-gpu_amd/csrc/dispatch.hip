@@ -40,6 +40,8 @@ void Workspace::release_all() {
 // (G lanes per pair, R rows per lane) shapes: query rows covered = G*R.
 struct Shape { int G, R; };
 static const Shape kShapes[] = {{8, 8}, {8, 12}, {8, 16}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
+// packed kernel: R = 19 fits a 150-bp query (152 padded rows) exactly
+static const Shape kShapes16[] = {{8, 8}, {8, 12}, {8, 16}, {8, 19}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
 
 using WfFn = void (*)(WfArgs);
 
@@ -60,7 +62,7 @@ static WfFn wf_lookup(int algo, bool keys, bool tb, int G, int R) {
 
 static WfFn wf16_lookup(int G, int R) {
 #define GX_CASE(g, r) if (G == g && R == r) return &wf16_local_kernel<g, r>;
-    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 20)
     GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
 #undef GX_CASE
     return nullptr;
@@ -73,7 +75,9 @@ static bool packed16_ok(const gasalx_params &p, uint32_t mq, uint32_t mt) {
     if (p.algo != 3 || p.second_best || p.start_pos != 0) return false;
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
-    if (p.gap_open + p.gap_extend > 16000 || p.mismatch > 16000) return false;
+    if (p.gap_open + p.gap_extend > 16000 || p.match + p.mismatch > 255) return false;
+    if (p.has_n_penalty && p.match + p.n_penalty > 255) return false;   // fast-path table bytes
+    if (p.has_n_penalty && p.n_penalty > 16000) return false;
     if ((int64_t)p.match * std::min(mq, mt) > 255) return false;
     return pad8(mt) <= 256;
 }
@@ -119,8 +123,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         pl.need_pack = has_ops;
         pl.packed16 = packed16_ok(p, s.max_q, s.max_t);
         if (pl.packed16) {
+            for (const Shape &sh : kShapes16)
+                if ((uint32_t)(sh.G * sh.R) >= q8) { pl.G = sh.G; pl.R = sh.R; break; }
             const uint32_t words = (t8 + 2 * pl.G + 4 + 3) & ~3u;   // odd-step tail + prefetch
-            pl.lds_stride = words * 4;
+            pl.lds_stride = words * 8;                              // uint2 per column
             pl.lds_bytes = (size_t)kWavesPerBlock * (64 / pl.G) * pl.lds_stride;
         }
         const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";

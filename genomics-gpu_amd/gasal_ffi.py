@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgasal.so")
+LIB_PATH = os.environ.get("GASALX_LIB") or os.path.join(_HERE, "lib", "libgasal.so")
 
 # enum values of the reference (gasal.h:37-73)
 WITHOUT_START, WITH_START, WITH_TB = 0, 1, 2

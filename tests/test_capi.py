@@ -62,7 +62,7 @@ def test_decode_cigar_merges_split_runs():
 
 
 def test_plan_selection_cpu_only():
-    assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150) == "wavefront16_local_G8R20"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150) == "wavefront16_local_G8R19"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, match=2), 150, 150) == "wavefront_local_keys_G8R20"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB), 150, 150) == "wavefront_local_tb_keys_G8R20"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, second_best=1), 150, 150) == "generic_local"
