@@ -236,6 +236,11 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.lds_stride = pl.lds_stride;
         A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
         A.one = 0x00010001u;
+        if (pl.packed16) {   // value range of the fast path (wavefront16.hpp, fast16_params)
+            const int64_t k = std::max(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
+            const int64_t base = 0x400 + p.gap_open + p.gap_extend + k + 16;
+            A.fast16 = (p.match + k <= 255 && base + 255 + p.match + k <= 0x7BFF) ? 1 : 0;
+        }
         WfFn fn = pl.packed16 ? wf16_lookup(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
         if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds_bytes > 64 * 1024)

@@ -41,6 +41,7 @@ struct WfArgs {
     uint32_t lds_stride;       // bytes of LDS per pair slot (>= max padded target + 4)
     int32_t force_exact;       // always take the exact-N substitution path
     uint32_t one;              // 0x00010001 (opaque to the compiler, see wavefront16.hpp)
+    int32_t fast16;            // wavefront16: the offset range of the perm/max3 fast path holds
 };
 
 constexpr int kWavesPerBlock = 4;

@@ -188,20 +188,30 @@ __device__ __forceinline__ void wf16_body(const WfArgs &A, const uint2 *tcol, co
 }
 
 // ---------------------------------------------------------------------------
-// Fast path (every code of the block is A/C/G/T, query N only in pad rows):
-// the substitution score comes from one v_perm_b32 per row.  Each column of
-// the staged target holds two 4-byte tables T0/T1 (pair 0 / pair 1) with
-// byte j = score(query letter j, target) + K >= 0; the row's selector picks
-// byte l0 of T0 for the low half and byte 4+l1 of T1 for the high half (bytes
-// 1 and 3 select the constant 0).  tmp = H + v - K is then one v_add_u32 and
-// one saturating v_pk_sub_i16: with H stored as H + 0x8000 the signed
-// saturation at -32768 IS the local floor at 0, so tmp, and therefore H,
-// never drop below the bias.  E and F are not floored (they stay above
-// 0x8000 - OE - e > 0, so their 32-bit subtractions never borrow either).
-// Per row: 7 half-rate + 4 full-rate instructions for two cells.
+// Fast path (every code of the block is A/C/G/T, query N only in pad rows).
+//
+// Substitution: each staged column holds two 4-byte tables T0/T1 (pair 0 /
+// pair 1), byte j = score(query letter j, target) + K >= 0; one v_perm_b32
+// per row picks byte l0 of T0 into the low half and byte 4+l1 of T1 into the
+// high half (selector bytes 1 and 3 = 0x0C give 0).
+//
+// Representation: every DP value is stored as value + B with B chosen so that
+// all stored values stay inside the positive, normal f16 range
+// [0x0400, 0x7BFF], where the f16 order of the bit patterns equals their
+// integer order — so v_pk_maximum3_f16 is an exact 3-way integer max on both
+// halves (bit patterns in, one of them out):
+//   t1 = diag + v;  tmp = t1 - K;  H = max3(tmp, F, E)
+//   toe = t1 - (OE + K);  E' = max3(toe, E - e, B);  F' = max3(toe, F - e, B)
+// (GASAL2's local core, local_kernel_template.h:19-30; flooring E and F at 0
+// is exact: values below 0 never reach H, and H >= 0 follows).  Adds and
+// subtracts are 32-bit on the packed pair and never carry across bit 16.
+// Per row: perm, 5 add/sub, 3 maximum3 and the key mad + max = 11
+// instructions for two cells (the int16 general path below needs 14).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pk_subsat_i16(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, __builtin_elementwise_sub_sat(GX_AS(pk_s2, a), GX_AS(pk_s2, b)));
+__device__ __forceinline__ uint32_t pk_max3_f16bits(uint32_t a, uint32_t b, uint32_t c) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 x = GX_AS(h2, a), y = GX_AS(h2, b), z = GX_AS(h2, c);
+    return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
 // A/C/G/T nibble -> 0..3, N -> 4, anything else -> 5
@@ -212,22 +222,36 @@ __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
     return (uint32_t)(((lut | set) >> (4 * (nib & 15u))) & 15u);
 }
 
+// Offsets of the fast path (the host planner checks the range, dispatch.hip).
+struct Fast16 {
+    int32_t k;      // table offset, >= max(b, N penalty)
+    int32_t base;   // B: stored value of 0
+};
+__device__ __forceinline__ Fast16 fast16_params(const WfArgs &A) {
+    Fast16 F;
+    F.k = max(A.b, A.has_npen ? A.npen : 0);
+    F.base = 0x0400 + A.o + A.e + F.k + 16;
+    return F;
+}
+
 template <int R>
 __device__ __forceinline__ void wf16f_step(const uint2 T, const int32_t c, const uint32_t diag_top,
                                            const uint32_t f_top, const uint32_t (&qs)[R], const uint32_t (&Hin)[R],
                                            uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
-                                           uint32_t &f_out, const uint32_t OE, const uint32_t EXT, const uint32_t KK,
-                                           const uint32_t KMUL) {
-    const uint32_t invc = (c >= 0 && c < 256) ? (uint32_t)(255 - c) * 0x10001u : 0u;
+                                           uint32_t &f_out, const uint32_t KK, const uint32_t OEK, const uint32_t EXT,
+                                           const uint32_t BB, const uint32_t KMUL, const uint32_t bshift) {
+    const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
+    const uint32_t invc = ((col - bshift) & 0xFFFFu) * 0x10001u;   // key = H*256 + col (mod 2^16)
     uint32_t diag = diag_top, f = f_top;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, qs[k]);
-        const uint32_t tmp = pk_subsat_i16(pk_addnc(diag, v), KK);
-        const uint32_t H = pk_max_u16(pk_max_u16(tmp, f), Ek[k]);
-        const uint32_t toe = pk_subnb(tmp, OE);
-        Ek[k] = pk_max_u16(toe, pk_subnb(Ek[k], EXT));
-        f = pk_max_u16(toe, pk_subnb(f, EXT));
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KK);
+        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t H = pk_max3_f16bits(tmp, f, Ek[k]);
+        Ek[k] = pk_max3_f16bits(toe, pk_subnb(Ek[k], EXT), BB);
+        f = pk_max3_f16bits(toe, pk_subnb(f, EXT), BB);
         key[k] = pk_max_u16(key[k], pk_mad_u16(H, KMUL, invc));
         diag = Hin[k];
         Hout[k] = H;
@@ -238,12 +262,13 @@ __device__ __forceinline__ void wf16f_step(const uint2 T, const int32_t c, const
 template <int G, int R>
 __device__ __forceinline__ void wf16f_body(const WfArgs &A, const uint2 *tcol, const uint32_t lg,
                                            const uint32_t nsteps, const uint32_t (&qs)[R], uint32_t (&key)[R]) {
-    const uint32_t BB = kPkBias * 0x10001u;
-    const uint32_t OE = pk_bcast(A.o + A.e);
+    const Fast16 P = fast16_params(A);
+    const uint32_t BB = (uint32_t)P.base * 0x10001u;
+    const uint32_t KK = pk_bcast(P.k);
+    const uint32_t OEK = pk_bcast(A.o + A.e + P.k);
     const uint32_t EXT = pk_bcast(A.e);
-    const int32_t K = max(A.b, A.has_npen ? A.npen : 0);
-    const uint32_t KK = pk_bcast(K);
     const uint32_t KMUL = A.one << 8;
+    const uint32_t bshift = ((uint32_t)P.base << 8) & 0xFFFFu;
     uint32_t HA[R], HB[R], Ek[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
@@ -254,13 +279,15 @@ __device__ __forceinline__ void wf16f_body(const WfArgs &A, const uint2 *tcol, c
     for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
         uint2 T = tnext;
         tnext = tcol[c + 1 + G];
-        wf16f_step<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, qs, HA, HB, Ek, key, f, OE, EXT, KK, KMUL);
+        wf16f_step<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, qs, HA, HB, Ek, key, f, KK, OEK, EXT, BB, KMUL,
+                      bshift);
         prevRecvH = recvH;
         recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
         recvF = (uint32_t)shr_lane((int32_t)f);
         T = tnext;
         tnext = tcol[c + 2 + G];
-        wf16f_step<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, qs, HB, HA, Ek, key, f, OE, EXT, KK, KMUL);
+        wf16f_step<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, qs, HB, HA, Ek, key, f, KK, OEK, EXT, BB,
+                      KMUL, bshift);
         prevRecvH = recvH;
         recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
         recvF = (uint32_t)shr_lane((int32_t)f);
@@ -338,15 +365,16 @@ __global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_local_kernel(WfArg
             }
         }
     }
-    const bool fast = !A.force_exact && !__syncthreads_or(other);
+    const bool fast = A.fast16 && !A.force_exact && !__syncthreads_or(other);
     const uint32_t nsteps = tmaxw + G - 1;
     const uint2 *tcol = wl + slot * words;
     uint32_t key[R];
     if (fast) {
-        // codes -> per-column score tables (byte j = score(letter j, t) + K)
-        const int32_t K = max(A.b, A.has_npen ? A.npen : 0);
+        // codes -> per-column score tables (byte j = score(letter j, t) + Kt; Kt outside the grid)
+        const int32_t K = fast16_params(A).k;
         const int32_t NS = A.has_npen ? -A.npen : 0;
         const uint32_t mis = (uint32_t)(K - A.b) * 0x01010101u, nrow = (uint32_t)(NS + K) * 0x01010101u;
+        const uint32_t outside = (uint32_t)K * 0x01010101u;
         for (uint32_t e = lane; e < S * words; e += 64) {
             const uint32_t cw = wl[e].y;
             uint32_t tab[2];
@@ -354,8 +382,8 @@ __global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_local_kernel(WfArg
             for (int h = 0; h < 2; ++h) {
                 const uint32_t t = (cw >> (16 * h)) & 0xFFu;
                 const uint32_t l = t == 0xFFu ? 6u : letter_of(t, A.nval);
-                tab[h] = l == 6 ? 0u : l == 4 ? nrow
-                                             : (mis & ~(0xFFu << (8 * l))) | ((uint32_t)(A.a + K) << (8 * l));
+                tab[h] = l == 6 ? outside : l == 4 ? nrow
+                                                   : (mis & ~(0xFFu << (8 * l))) | ((uint32_t)(A.a + K) << (8 * l));
             }
             wl[e] = make_uint2(tab[0], tab[1]);
         }
