@@ -26,7 +26,9 @@ sys.path.insert(0, os.path.join(ROOT, "genomics-gpu_amd"))
 import gasal_ffi as G  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
+# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles (full-rate ops;
+# v_pk_*, max/min_32, perm, maximum3 issue at 4 — profiles/r01_valu_issue_rates.md)
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
 
 WORKLOADS = {
     # name: (synth kind, default pairs, params, algorithmic bytes per pair, int ops per cell, label)
@@ -48,6 +50,8 @@ def parse():
     ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: all-gather every rank's int32 scores (RCCL) inside each timed step")
     return ap.parse_args()
 
 
@@ -112,8 +116,12 @@ def main():
     torch.cuda.set_stream(stream)
     maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
 
+    gathered = [torch.empty_like(d["aln_score"]) for _ in range(world)] if (args.gather and world > 1) else None
+
     def step():
         eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, maxq, maxt, stream.cuda_stream)
+        if gathered is not None:   # optional exchange step of SURVEY §8(e): every rank gets all scores
+            dist.all_gather(gathered, d["aln_score"])
 
     for _ in range(args.warmup):
         step()
@@ -143,7 +151,22 @@ def main():
         gcups = total_cells / elapsed / 1e9
         kern_s = kern_ms / 1e3
         achieved = bytes_per_pair * n / kern_s / 1e9
-        valu = ops_per_cell * cells_per_step / kern_s
+        plan = G.describe_plan(params, maxq, maxt)
+        valu_roof = None
+        census_path = os.path.join(ROOT, "profiles", "isa_census.json")
+        if os.path.exists(census_path):
+            cen = json.load(open(census_path)).get(plan)
+            if cen:
+                gsz, ppl = cen["G"], cen["pairs_per_lane"]
+                waves = -(-n // (ppl * (64 // gsz)))
+                steps = (maxt + 7) // 8 * 8 + gsz - 1
+                steps += steps % cen["steps_per_iteration"]
+                instr = waves * steps * cen["valu_per_step"]
+                ach = instr / kern_s
+                valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e12, 4), "peak": VALU_PEAK_WAVE_INSTR / 1e12,
+                             "unit": "T wave-instr/s", "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
+                             "valu_per_step": cen["valu_per_step"], "rows_per_lane": cen["R"],
+                             "pairs_per_lane": ppl, "source": "profiles/isa_census.json (tools/isa_census.py)"}
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
         if os.path.exists(pmc_path):
@@ -165,12 +188,12 @@ def main():
             "dtype": "int32",
             "data": "synthetic (SURVEY.md 8(d) generator, std::mt19937_64), resident in HBM",
             "config": {"workload": label, "pairs_per_gpu": n, "cells_per_gpu_step": cells_per_step,
-                       "plan": G.describe_plan(params, maxq, maxt), "parallelism": f"dp{world} (pairs sharded)"},
+                       "plan": plan,
+                       "parallelism": f"dp{world} (pairs sharded)" + (", all-gather of scores" if gathered else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "bytes_per_pair": bytes_per_pair, "kernel_ms": round(kern_ms, 4)},
-            "valu_roofline": {"bound": "valu-int32", "achieved": round(valu / 1e12, 3), "peak": VALU_PEAK_OPS / 1e12,
-                              "unit": "Tops/s", "frac": round(valu / VALU_PEAK_OPS, 4), "ops_per_cell": ops_per_cell},
+            "valu_roofline": valu_roof,
             "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
