@@ -153,27 +153,21 @@ def main():
         achieved = bytes_per_pair * n / kern_s / 1e9
         plan = G.describe_plan(params, maxq, maxt)
         valu_roof = None
-        census_path = os.path.join(ROOT, "profiles", "isa_census.json")
-        if os.path.exists(census_path):
-            cen = json.load(open(census_path)).get(plan)
-            if cen:
-                gsz, ppl = cen["G"], cen["pairs_per_lane"]
-                waves = -(-n // (ppl * (64 // gsz)))
-                steps = (maxt + 7) // 8 * 8 + gsz - 1
-                steps += steps % cen["steps_per_iteration"]
-                instr = waves * steps * cen["valu_per_step"]
-                ach = instr / kern_s
-                valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e12, 4), "peak": VALU_PEAK_WAVE_INSTR / 1e12,
-                             "unit": "T wave-instr/s", "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
-                             "valu_per_step": cen["valu_per_step"], "rows_per_lane": cen["R"],
-                             "pairs_per_lane": ppl, "source": "profiles/isa_census.json (tools/isa_census.py)"}
-        traffic = None
+        pmc = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
         if os.path.exists(pmc_path):
             try:
-                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
+                pmc = json.load(open(pmc_path))
             except Exception:
-                traffic = None
+                pmc = None
+        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        if pmc and pmc.get("valu_insts_per_launch") and pmc.get("pairs_per_launch", n) == n:
+            # dynamic VALU wave-instructions of the dominant kernel (SQ_INSTS_VALU, same workload)
+            ach = pmc["valu_insts_per_launch"] / kern_s
+            valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e12, 4), "peak": VALU_PEAK_WAVE_INSTR / 1e12,
+                         "unit": "T wave-instr/s", "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
+                         "valu_insts_per_launch": pmc["valu_insts_per_launch"],
+                         "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU)"}
         out = {
             "metric": "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %",
             "value": round(gcups, 2),

@@ -40,8 +40,10 @@ void Workspace::release_all() {
 // (G lanes per pair, R rows per lane) shapes: query rows covered = G*R.
 struct Shape { int G, R; };
 static const Shape kShapes[] = {{8, 8}, {8, 12}, {8, 16}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
-// packed kernel: R = 19 fits a 150-bp query (152 padded rows) exactly
-static const Shape kShapes16[] = {{8, 8}, {8, 12}, {8, 16}, {8, 19}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
+// packed kernels (register axis = query for LOCAL/GLOBAL, target for SEMI):
+// R = 19 fits 150 bp (152 padded) and R = 23 fits 182 bp (184 padded) exactly
+static const Shape kShapes16[] = {{8, 8},   {8, 12},  {8, 16},  {8, 19},  {8, 20},
+                                  {8, 23},  {16, 16}, {16, 20}, {32, 20}, {64, 20}};
 
 using WfFn = void (*)(WfArgs);
 
@@ -60,26 +62,55 @@ static WfFn wf_lookup(int algo, bool keys, bool tb, int G, int R) {
     return keys ? wf_pick<WF_SEMI, true, false>(G, R) : wf_pick<WF_SEMI, false, false>(G, R);
 }
 
-static WfFn wf16_lookup(int G, int R) {
-#define GX_CASE(g, r) if (G == g && R == r) return &wf16_local_kernel<g, r>;
-    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 20)
+template <int ALGO>
+static WfFn wf16_pick(int G, int R) {
+#define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<ALGO, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 20) GX_CASE(8, 23)
     GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
 #undef GX_CASE
     return nullptr;
 }
 
+static WfFn wf16_lookup(int algo, int G, int R) {
+    if (algo == WF_LOCAL) return wf16_pick<WF_LOCAL>(G, R);
+    if (algo == WF_GLOBAL) return wf16_pick<WF_GLOBAL>(G, R);
+    return wf16_pick<WF_SEMI>(G, R);
+}
+
 static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 
-// The packed kernel is exact when every DP value fits its 16-bit key field.
-static bool packed16_ok(const gasalx_params &p, uint32_t mq, uint32_t mt) {
-    if (p.algo != 3 || p.second_best || p.start_pos != 0) return false;
+// The packed kernels (wavefront16.hpp) are exact when every stored value stays
+// inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
+// fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
+static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
+    if (p.second_best || p.start_pos != 0) return false;
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
-    if (p.gap_open + p.gap_extend > 16000 || p.match + p.mismatch > 255) return false;
-    if (p.has_n_penalty && p.match + p.n_penalty > 255) return false;   // fast-path table bytes
-    if (p.has_n_penalty && p.n_penalty > 16000) return false;
-    if ((int64_t)p.match * std::min(mq, mt) > 255) return false;
-    return pad8(mt) <= 256;
+    const int64_t a = p.match, b = p.mismatch, oe = (int64_t)p.gap_open + p.gap_extend, e = p.gap_extend;
+    const int64_t npen = p.has_n_penalty ? p.n_penalty : 0;
+    const int64_t q8 = pad8(mq), t8 = pad8(mt);
+    if (wf_algo == WF_LOCAL) {
+        const int64_t k = std::max(b, npen);
+        if (a + k > 255 || a * std::min(mq, mt) > 255 || t8 > 256) return false;   // 16-bit key: H*256 + col
+        const int64_t base = 0x400 + oe + k + 16;
+        *vmin = 0;
+        return base + 255 + a + k + 64 <= 0x7BFF;
+    }
+    int64_t k, top;
+    if (wf_algo == WF_SEMI) {
+        if (p.tail != 2) return false;                         // TAIL=TARGET only (last query row)
+        if (oe < b || oe < npen) return false;                 // table offset K = OE
+        k = oe;
+    } else {
+        k = std::max(b, npen);
+    }
+    if (a + k > 255) return false;
+    const int64_t v = 4 * oe + k + e * (q8 + t8) + 64;         // below every reachable value
+    const int64_t neg = 0x400 + 2 * e + 16;
+    top = neg + v + a * std::min(q8, t8) + a + k + oe + 64;
+    if (top > 0x7BFF) return false;
+    *vmin = (int32_t)v;
+    return true;
 }
 
 // Largest |value| the DP can reach, to decide whether int32 arithmetic without
@@ -121,17 +152,23 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         pl.kind = PLAN_WAVEFRONT;
         pl.wf_algo = wf_algo; pl.keys = keys; pl.tb = tb && wf_algo != WF_SEMI;
         pl.need_pack = has_ops;
-        pl.packed16 = packed16_ok(p, s.max_q, s.max_t);
+        pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin);
         if (pl.packed16) {
+            const uint32_t x8 = (wf_algo == WF_SEMI) ? t8 : q8, y8 = (wf_algo == WF_SEMI) ? q8 : t8;
+            pl.G16 = 0;
             for (const Shape &sh : kShapes16)
-                if ((uint32_t)(sh.G * sh.R) >= q8) { pl.G = sh.G; pl.R = sh.R; break; }
-            const uint32_t words = (t8 + 2 * pl.G + 4 + 3) & ~3u;   // odd-step tail + prefetch
-            pl.lds_stride = words * 8;                              // uint2 per column
-            pl.lds_bytes = (size_t)kWavesPerBlock * (64 / pl.G) * pl.lds_stride;
+                if ((uint32_t)(sh.G * sh.R) >= x8) { pl.G16 = sh.G; pl.R16 = sh.R; break; }
+            const uint32_t words = (y8 + 2 * pl.G16 + 4 + 3) & ~3u;   // odd-step tail + prefetch
+            pl.lds16_stride = words * 8;                               // uint2 per position
+            pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
+            if (pl.G16 == 0 || pl.lds16_bytes > 160 * 1024) pl.packed16 = false;
         }
         const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";
-        pl.name = std::string(pl.packed16 ? "wavefront16_" : "wavefront_") + an + (pl.tb ? "_tb" : "") +
-                  (keys && !pl.packed16 ? "_keys" : "") + "_G" + std::to_string(pl.G) + "R" + std::to_string(pl.R);
+        if (pl.packed16)
+            pl.name = std::string("wavefront16_") + an + "_G" + std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
+        else
+            pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
+                      std::to_string(pl.G) + "R" + std::to_string(pl.R);
     } else if (p.algo == 1 || p.algo == 2 || p.algo == 3 || p.algo == 5 || p.algo == 6) {
         pl.kind = PLAN_GENERIC;
         pl.need_pack = true;
@@ -236,17 +273,32 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.lds_stride = pl.lds_stride;
         A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
         A.one = 0x00010001u;
-        if (pl.packed16) {   // value range of the fast path (wavefront16.hpp, fast16_params)
-            const int64_t k = std::max(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
-            const int64_t base = 0x400 + p.gap_open + p.gap_extend + k + 16;
-            A.fast16 = (p.match + k <= 255 && base + 255 + p.match + k <= 0x7BFF) ? 1 : 0;
+        if (pl.packed16) {
+            // packed kernel first; it marks every block it aligned in ws.misc ...
+            WfArgs P16 = A;
+            P16.lds_stride = pl.lds16_stride;
+            P16.fast16 = 1;
+            P16.vmin = pl.vmin;
+            const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
+            const uint32_t grid16 = grid_for(n, ppb16);
+            HIPCHK(ws.misc.reserve(grid16 + 64));
+            P16.handled = ws.misc.as<uint8_t>();
+            WfFn f16 = wf16_lookup(pl.wf_algo, pl.G16, pl.R16);
+            if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
+            if (pl.lds16_bytes > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)pl.lds16_bytes));
+            hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
+            HIPCHK(hipGetLastError());
+            // ... and the int32 kernel aligns the pairs of the blocks it declined
+            A.skip = ws.misc.as<uint8_t>();
+            A.skip_ppb = ppb16;
         }
-        WfFn fn = pl.packed16 ? wf16_lookup(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+        WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
         if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
-        const uint32_t pairs_per_block = kWavesPerBlock * (64 / pl.G) * (pl.packed16 ? 2 : 1);
-        hipLaunchKernelGGL(fn, dim3(grid_for(n, pairs_per_block)), dim3(kBlock), pl.lds_bytes, st, A);
+        hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
         HIPCHK(hipGetLastError());
     } else {
         GenArgs A;

@@ -29,7 +29,7 @@ struct Workspace {
     DevBuf tb;                      // traceback direction words
     DevBuf rows_h, rows_e, rev;     // generic kernels' row buffers
     DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
-    DevBuf misc;                    // device-side max reduction
+    DevBuf misc;                    // packed kernels: per-block "aligned here" flags
     void release_all();
 };
 
@@ -39,7 +39,11 @@ struct Plan {
     PlanKind kind = PLAN_NONE;
     int wf_algo = 0;        // WfAlgo
     bool keys = false, tb = false;
-    bool packed16 = false;  // two pairs per lane in int16 halves (wavefront16.hpp)
+    bool packed16 = false;  // two pairs per lane in 16-bit halves (wavefront16.hpp), int32 fallback
+    int G16 = 0, R16 = 0;   // packed kernel shape
+    uint32_t lds16_stride = 0;
+    size_t lds16_bytes = 0;
+    int32_t vmin = 0;       // packed GLOBAL/SEMI value-range bound
     int G = 0, R = 0;
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;

@@ -41,7 +41,12 @@ struct WfArgs {
     uint32_t lds_stride;       // bytes of LDS per pair slot (>= max padded target + 4)
     int32_t force_exact;       // always take the exact-N substitution path
     uint32_t one;              // 0x00010001 (opaque to the compiler, see wavefront16.hpp)
-    int32_t fast16;            // wavefront16: the offset range of the perm/max3 fast path holds
+    int32_t fast16;            // wavefront16: the value range of the packed path holds (planner)
+    int32_t vmin;              // wavefront16 GLOBAL/SEMI: bound on |lowest reachable value| (planner)
+    uint8_t *handled;          // wavefront16: per block, 1 = aligned here, 0 = left to the int32 kernel
+    const uint8_t *skip;       // int32 kernel: pairs whose packed block already aligned them
+    uint32_t skip_ppb;         // pairs per packed block
+
 };
 
 constexpr int kWavesPerBlock = 4;
@@ -313,7 +318,9 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     const uint32_t slot = lane / G;
     const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * P;
     const uint32_t pair = pair0 + slot;
-    const bool valid = pair < A.n;
+    // pairs the packed kernel already aligned are skipped (dispatch.hip)
+    const bool valid = pair < A.n && !(A.skip && A.skip[pair / A.skip_ppb]);
+    if (A.skip && !__syncthreads_or(valid)) return;      // block-uniform early exit
 
     uint32_t ql = 0, tl = 0, qo = 0, to = 0;
     if (valid) { ql = A.qlen[pair]; tl = A.tlen[pair]; qo = A.qoff[pair]; to = A.toff[pair]; }

@@ -1,36 +1,47 @@
-// wavefront16.hpp — packed-int16 segmented wavefront for LOCAL score + ends.
+// wavefront16.hpp — packed two-pairs-per-lane wavefront kernels (LOCAL, GLOBAL,
+// SEMI-GLOBAL score paths) for gfx950.
 //
-// Same sweep as wavefront.hpp (G lanes per group, R query rows per lane, one
-// column per step, DPP wave_shr:1 hand-off), but every VGPR holds TWO pairs:
-// the low 16 bits belong to pair 2*slot and the high 16 bits to pair
-// 2*slot+1.  The cell update is GASAL2's CORE_LOCAL_COMPUTE
-// (local_kernel_template.h:19-30):
-//   tmp = H(r-1,c-1) + s;  H = max(tmp, F, E, 0);
-//   E'  = max(tmp - OE, E - e);  F' = max(tmp - OE, F - e)
+// Sweep: as wavefront.hpp — a group of G lanes owns a DP matrix; lane lg holds
+// R consecutive positions of the "register axis" sequence X and, at step s,
+// computes position y = s - lg of the "step axis" sequence Y for all its R
+// positions, top to bottom; the last position's values go to lane lg+1 by DPP
+// wave_shr:1.  Every VGPR holds TWO pairs: low 16 bits pair 2*slot, high 16
+// bits pair 2*slot+1.
+//   LOCAL, GLOBAL: X = query (rows), Y = target (columns) — the reference's
+//                  orientation (local_kernel_template.h, global.h).
+//   SEMI:          X = target, Y = query (transposed), so that the last query
+//                  row — the only row the TAIL=TARGET result reads
+//                  (semiglobal_kernel_template.h:160-178) — is one step, read
+//                  once, instead of a per-cell running key.
 //
-// Instruction economics on gfx950 (tools/ubench_ops.hip, measured): every
-// v_pk_* op, v_max/min_*32, v_bitop3 and DPP issue at 4 cycles per wave64,
-// while v_add_u32 / v_sub_u32 / v_and / v_xor issue at 2.  So the cell is
-// written to use 32-bit adds/subtracts on the packed pair wherever no carry
-// or borrow can cross from the low half into the high half:
-//   * every DP value is stored with a bias B = 0x8000 (H = 0 <-> B), and the
-//     local floor is applied once per cell on tmp - OE (toe = max(., B)), so
-//     E and F never drop below B (max(E,0) obeys the same recurrence when
-//     e >= 0, and values below 0 never reach H): all four subtractions are
-//     borrow-free v_sub_u32;
-//   * the substitution score is s = M_c - min(x, AB_c) where x = (q ^ t) &
-//     mask holds the two codes' nibble at bit 8 or 12 of each half (so a
-//     mismatch gives x >= 256 >= AB_c = a + b), M_c / AB_c are per-column
-//     constants (a / a+b for bases, N rule / 0 for N columns, 0 / 0 outside
-//     the grid): one v_bitop3, one v_pk_min_u16, then tmp = diag - m + M_c.
-// Per row: 9 half-rate + 4 full-rate instructions for two cells.  The per-row
-// maximum is a 16-bit key (H << 8 | 255 - c), unaffected by the bias since
-// B * 256 = 0 mod 2^16; the strip-major first maximum is resolved
-// at the end exactly as in the int32 kernel.
+// Substitution: the step-axis sequence is staged in LDS as per-position score
+// tables, two 4-byte tables per uint2 (pair 0 / pair 1): byte j =
+// score(X letter j, Y code) + K >= 0.  One v_perm_b32 per cell-pair picks byte
+// l0 of table 0 into the low half and byte 4+l1 of table 1 into the high half
+// (selector bytes 1 and 3 = 0x0C give 0).  Blocks with codes other than
+// A/C/G/T on the register axis (or other than A/C/G/T/N on the step axis) are
+// declined: the kernel marks them in `handled` and the int32 kernel
+// (wavefront.hpp) aligns exactly those pairs afterwards (dispatch.hip).
 //
-// Exactness domain (checked by the planner, packed16_ok): every H <= 255
-// (a * min(ql,tl)), padded targets <= 256 columns, a + b <= 256, e >= 0,
-// o + e <= 16000, N penalty <= 16000.
+// Arithmetic: every stored DP value is value + B with B chosen so that all
+// stored values stay inside the positive, normal f16 range [0x0400, 0x7BFF],
+// where the f16 order of the bit patterns equals their integer order — so
+// v_pk_maximum3_f16 is an exact 3-way integer max on both halves, and 32-bit
+// adds/subtracts on the packed pair never carry across bit 16.  Issue cost on
+// gfx950 (profiles/r01_valu_issue_rates.md): v_pk_*, maximum3 and v_perm issue
+// at 4 cycles per wave64, v_add/sub_u32 at 2.
+//
+//   LOCAL  (local_kernel_template.h:19-30; floors at B are exact because
+//           values below 0 never reach H):
+//     t1 = diag + v; tmp = t1 - K; toe = t1 - (OE + K); H = max3(tmp, F, E)
+//     E' = max3(toe, E - e, B); F' = max3(toe, F - e, B); key = max(key, H*256 + 255-c)
+//     11 instructions per two cells.
+//   GLOBAL (global.h:4-12; the NEG floors never bind for reachable values):
+//     same without the key and with NEG in place of B: 9 instructions.
+//   SEMI   (semiglobal_kernel_template.h:17-28, H-based Gotoh; values stored
+//           as H - OE and the table offset K = OE folds the + OE):
+//     tmp = diag + v; F = max(Hup, F - e); E = max(Hleft, E - e);
+//     H' = max3(tmp, F, E) - OE: 8 instructions.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,180 +50,30 @@
 
 namespace gx {
 
-typedef short pk_s2 __attribute__((ext_vector_type(2)));
 typedef unsigned short pk_u2 __attribute__((ext_vector_type(2)));
 #define GX_AS(T, x) __builtin_bit_cast(T, x)
 
-// Plain vector expressions; the "1" of pk_min_u16 arrives as a kernel
-// argument so the compiler cannot turn min(x,1)*D + M into compare/select.
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
-}
 __device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {
     return GX_AS(uint32_t, GX_AS(pk_u2, a) * GX_AS(pk_u2, b) + GX_AS(pk_u2, c));
-}
-__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, __builtin_elementwise_max(GX_AS(pk_s2, a), GX_AS(pk_s2, b)));
 }
 __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
     return GX_AS(uint32_t, __builtin_elementwise_max(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
 }
-__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {   // max(a - b, 0), a,b >= 0
-    return GX_AS(uint32_t, __builtin_elementwise_sub_sat(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
-}
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, GX_AS(pk_s2, a) + GX_AS(pk_s2, b));
-}
-__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, GX_AS(pk_s2, a) - GX_AS(pk_s2, b));
-}
 // 32-bit add/sub used on a packed pair; exact per half when no carry/borrow
-// crosses bit 16 (guaranteed by the bias invariants above).
+// crosses bit 16 (guaranteed by the value-range invariants above).
 __device__ __forceinline__ uint32_t pk_addnc(uint32_t a, uint32_t b) { return a + b; }
 __device__ __forceinline__ uint32_t pk_subnb(uint32_t a, uint32_t b) { return a - b; }
 __device__ __forceinline__ uint32_t pk_bcast(int32_t v) { return ((uint32_t)v & 0xFFFFu) * 0x10001u; }
-
-#ifndef GX_WF16_PINGPONG
-#define GX_WF16_PINGPONG 1
-#endif
-#ifndef GX_WF16_WAVES
-#define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
-#endif
-
-constexpr uint32_t kPkInvalid = 0xFFu;   // target/query code outside the padded grid
-constexpr uint32_t kPkBias = 0x8000u;    // stored value of H = 0
-
-// Per-column constants of one step (both halves).
-struct Col16 {
-    uint32_t trep;   // target nibble at bits 8 and 12 of each half
-    uint32_t ab;     // a + b for a base column, 0 for N / outside
-    uint32_t m;      // a for a base column, N rule score for N, 0 outside
-    uint32_t qn;     // EXACT only: m - (N-row score) >= 0
-};
-
-template <bool NPEN, bool EXACT>
-__device__ __forceinline__ Col16 col16(const uint32_t t, const uint32_t NVALp, const uint32_t Ap, const uint32_t ABp,
-                                       const uint32_t NSp, const uint32_t ONEp) {
-    const uint32_t INVp = 0x00FF00FFu;
-    const uint32_t notN = pk_min_u16(t ^ NVALp, ONEp);
-    const uint32_t notI = pk_min_u16(t ^ INVp, ONEp);
-    const uint32_t live = pk_mad_u16(notN, notI, 0u);
-    Col16 C;
-    C.trep = pk_mad_u16(t & 0x000F000Fu, 0x11001100u, 0u);
-    C.ab = pk_mad_u16(live, ABp, 0u);
-    // N column: M = NS (<= 0), outside: 0, base: a
-    C.m = NPEN ? pk_mad_u16(notI, pk_mad_u16(notN, pk_sub(Ap, NSp), NSp), 0u)
-               : pk_mad_u16(live, Ap, 0u);
-    C.qn = 0;
-    if (EXACT) C.qn = pk_sub(C.m, pk_mad_u16(notI, NSp, 0u));   // base: a - NS, N col: 0, outside: 0
-    // opaque per-column constants: keeps the compiler from re-deriving them per row
-    asm volatile("" : "+v"(C.ab), "+v"(C.m), "+v"(C.qn));
-    return C;
-}
-
-// One column step: rows read the previous column's H from Hin and write the
-// new H to Hout (ping-pong arrays, so no register copies on the back edge).
-template <int R, bool NPEN, bool EXACT>
-__device__ __forceinline__ void wf16_step(const Col16 &C, const int32_t c, const uint32_t diag_top,
-                                          const uint32_t f_top, const uint32_t (&qp)[(R + 1) / 2],
-                                          const uint32_t (&Hin)[R], uint32_t (&Hout)[R], uint32_t (&Ek)[R],
-                                          uint32_t (&key)[R], uint32_t &f_out, const uint32_t OE,
-                                          const uint32_t EXT, const uint32_t NREP, const uint32_t ONEp) {
-    const uint32_t BB = kPkBias * 0x10001u;
-    const bool kc = c >= 0 && c < 256;
-    const uint32_t invc = kc ? pk_bcast(255 - c) : 0u;
-    const uint32_t kmul = kc ? (ONEp << 8) : 0u;                  // key = H*256 + 255-c
-    uint32_t diag = diag_top, f = f_top;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const uint32_t mask = 0x0F000F00u << (4 * (k & 1));
-        const uint32_t q = qp[k >> 1];
-        uint32_t m = pk_min_u16((q ^ C.trep) & mask, C.ab);
-        if (EXACT) {   // query N (LOCAL N rule): m = qn for that row
-            const uint32_t notNq = pk_min_u16((q ^ NREP) & mask, ONEp);
-            m = pk_mad_u16(notNq, pk_sub(m, C.qn), C.qn);
-        }
-        const uint32_t tmp = NPEN ? pk_add(pk_subnb(diag, m), C.m) : pk_addnc(pk_subnb(diag, m), C.m);
-        const uint32_t H = pk_max_u16(pk_max_u16(tmp, f), Ek[k]);
-        const uint32_t toe = pk_max_u16(pk_subnb(tmp, OE), BB);
-        Ek[k] = pk_max_u16(toe, pk_subnb(Ek[k], EXT));
-        f = pk_max_u16(toe, pk_subnb(f, EXT));
-        key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmul, invc));
-        diag = Hin[k];
-        Hout[k] = H;
-    }
-    f_out = f;
-}
-
-template <int G, int R, bool NPEN, bool EXACT>
-__device__ __forceinline__ void wf16_body(const WfArgs &A, const uint2 *tcol, const uint32_t lg,
-                                          const uint32_t nsteps, const uint32_t (&qp)[(R + 1) / 2],
-                                          uint32_t (&key)[R]) {
-    const uint32_t BB = kPkBias * 0x10001u;
-    const uint32_t OE = pk_bcast(A.o + A.e);
-    const uint32_t EXT = pk_bcast(A.e);
-    const uint32_t NVALp = pk_bcast(A.nval);
-    const uint32_t NREP = pk_bcast(A.nval * 0x1100);
-    const int32_t NS = A.has_npen ? -A.npen : 0;
-    const uint32_t Ap = pk_bcast(A.a), NSp = pk_bcast(NS), ABp = pk_bcast(A.a + A.b);
-    const uint32_t ONEp = A.one;
-    uint32_t HA[R], Ek[R];
-#if GX_WF16_PINGPONG
-    uint32_t HB[R];
-#else
-    uint32_t (&HB)[R] = HA;   // one array: the compiler renames with a copy per row
-#endif
-#pragma unroll
-    for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
-    uint32_t recvH = BB, prevRecvH = BB, recvF = BB, f = BB;
-    const bool top = lg == 0;
-    int32_t c = -(int32_t)lg;
-    uint32_t tnext = tcol[c + G].y;
-    // two columns per iteration (the odd tail step reads only "outside" columns)
-    for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-        Col16 C = col16<NPEN, EXACT>(tnext, NVALp, Ap, ABp, NSp, ONEp);
-        tnext = tcol[c + 1 + G].y;
-        wf16_step<R, NPEN, EXACT>(C, c, top ? BB : prevRecvH, top ? BB : recvF, qp, HA, HB, Ek, key, f, OE, EXT,
-                                  NREP, ONEp);
-        prevRecvH = recvH;
-        recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
-        recvF = (uint32_t)shr_lane((int32_t)f);
-        C = col16<NPEN, EXACT>(tnext, NVALp, Ap, ABp, NSp, ONEp);
-        tnext = tcol[c + 2 + G].y;
-        wf16_step<R, NPEN, EXACT>(C, c + 1, top ? BB : prevRecvH, top ? BB : recvF, qp, HB, HA, Ek, key, f, OE,
-                                  EXT, NREP, ONEp);
-        prevRecvH = recvH;
-        recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
-        recvF = (uint32_t)shr_lane((int32_t)f);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Fast path (every code of the block is A/C/G/T, query N only in pad rows).
-//
-// Substitution: each staged column holds two 4-byte tables T0/T1 (pair 0 /
-// pair 1), byte j = score(query letter j, target) + K >= 0; one v_perm_b32
-// per row picks byte l0 of T0 into the low half and byte 4+l1 of T1 into the
-// high half (selector bytes 1 and 3 = 0x0C give 0).
-//
-// Representation: every DP value is stored as value + B with B chosen so that
-// all stored values stay inside the positive, normal f16 range
-// [0x0400, 0x7BFF], where the f16 order of the bit patterns equals their
-// integer order — so v_pk_maximum3_f16 is an exact 3-way integer max on both
-// halves (bit patterns in, one of them out):
-//   t1 = diag + v;  tmp = t1 - K;  H = max3(tmp, F, E)
-//   toe = t1 - (OE + K);  E' = max3(toe, E - e, B);  F' = max3(toe, F - e, B)
-// (GASAL2's local core, local_kernel_template.h:19-30; flooring E and F at 0
-// is exact: values below 0 never reach H, and H >= 0 follows).  Adds and
-// subtracts are 32-bit on the packed pair and never carry across bit 16.
-// Per row: perm, 5 add/sub, 3 maximum3 and the key mad + max = 11
-// instructions for two cells (the int16 general path below needs 14).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pk_max3_f16bits(uint32_t a, uint32_t b, uint32_t c) {
+// exact integer 3-way max of bit patterns in [0x0400, 0x7BFF] (positive normal f16)
+__device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) {
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const h2 x = GX_AS(h2, a), y = GX_AS(h2, b), z = GX_AS(h2, c);
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
+
+#ifndef GX_WF16_WAVES
+#define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
+#endif
 
 // A/C/G/T nibble -> 0..3, N -> 4, anything else -> 5
 __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
@@ -222,21 +83,35 @@ __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
     return (uint32_t)(((lut | set) >> (4 * (nib & 15u))) & 15u);
 }
 
-// Offsets of the fast path (the host planner checks the range, dispatch.hip).
-struct Fast16 {
-    int32_t k;      // table offset, >= max(b, N penalty)
-    int32_t base;   // B: stored value of 0
+// Value-range constants of one launch (dispatch.hip packed16_ok checks that the
+// stored values stay inside [0x0400, 0x7BFF] for these).
+struct Pk16 {
+    int32_t k;      // table offset
+    int32_t base;   // stored value of 0
+    int32_t neg;    // stored "minus infinity" (below every reachable value)
 };
-__device__ __forceinline__ Fast16 fast16_params(const WfArgs &A) {
-    Fast16 F;
-    F.k = max(A.b, A.has_npen ? A.npen : 0);
-    F.base = 0x0400 + A.o + A.e + F.k + 16;
-    return F;
+template <int ALGO>
+__device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
+    Pk16 P;
+    const int32_t OE = A.o + A.e;
+    if (ALGO == WF_LOCAL) {
+        P.k = max(A.b, A.has_npen ? A.npen : 0);
+        P.base = 0x0400 + OE + P.k + 16;
+        P.neg = P.base;
+    } else {
+        P.k = (ALGO == WF_SEMI) ? OE : max(A.b, A.has_npen ? A.npen : 0);
+        P.neg = 0x0400 + 2 * A.e + 16;
+        P.base = P.neg + A.vmin;
+    }
+    return P;
 }
 
+// ---------------------------------------------------------------------------
+// LOCAL step: registers = query rows, one target column per step.
+// ---------------------------------------------------------------------------
 template <int R>
-__device__ __forceinline__ void wf16f_step(const uint2 T, const int32_t c, const uint32_t diag_top,
-                                           const uint32_t f_top, const uint32_t (&qs)[R], const uint32_t (&Hin)[R],
+__device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const uint32_t diag_top,
+                                           const uint32_t f_top, const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                            uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
                                            uint32_t &f_out, const uint32_t KK, const uint32_t OEK, const uint32_t EXT,
                                            const uint32_t BB, const uint32_t KMUL, const uint32_t bshift) {
@@ -245,13 +120,13 @@ __device__ __forceinline__ void wf16f_step(const uint2 T, const int32_t c, const
     uint32_t diag = diag_top, f = f_top;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, qs[k]);
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
         const uint32_t t1 = pk_addnc(diag, v);
         const uint32_t tmp = pk_subnb(t1, KK);
         const uint32_t toe = pk_subnb(t1, OEK);
-        const uint32_t H = pk_max3_f16bits(tmp, f, Ek[k]);
-        Ek[k] = pk_max3_f16bits(toe, pk_subnb(Ek[k], EXT), BB);
-        f = pk_max3_f16bits(toe, pk_subnb(f, EXT), BB);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), BB);
+        f = pk_max3(toe, pk_subnb(f, EXT), BB);
         key[k] = pk_max_u16(key[k], pk_mad_u16(H, KMUL, invc));
         diag = Hin[k];
         Hout[k] = H;
@@ -259,192 +134,344 @@ __device__ __forceinline__ void wf16f_step(const uint2 T, const int32_t c, const
     f_out = f;
 }
 
-template <int G, int R>
-__device__ __forceinline__ void wf16f_body(const WfArgs &A, const uint2 *tcol, const uint32_t lg,
-                                           const uint32_t nsteps, const uint32_t (&qs)[R], uint32_t (&key)[R]) {
-    const Fast16 P = fast16_params(A);
-    const uint32_t BB = (uint32_t)P.base * 0x10001u;
-    const uint32_t KK = pk_bcast(P.k);
-    const uint32_t OEK = pk_bcast(A.o + A.e + P.k);
-    const uint32_t EXT = pk_bcast(A.e);
-    const uint32_t KMUL = A.one << 8;
-    const uint32_t bshift = ((uint32_t)P.base << 8) & 0xFFFFu;
-    uint32_t HA[R], HB[R], Ek[R];
+// ---------------------------------------------------------------------------
+// GLOBAL step: as LOCAL without the floor at 0 and without keys.
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
+                                            const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
+                                            uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t KK,
+                                            const uint32_t OEK, const uint32_t EXT, const uint32_t NN) {
+    uint32_t diag = diag_top, f = f_top;
 #pragma unroll
-    for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
-    uint32_t recvH = BB, prevRecvH = BB, recvF = BB, f = BB;
-    const bool top = lg == 0;
-    int32_t c = -(int32_t)lg;
-    uint2 tnext = tcol[c + G];
-    for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-        uint2 T = tnext;
-        tnext = tcol[c + 1 + G];
-        wf16f_step<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, qs, HA, HB, Ek, key, f, KK, OEK, EXT, BB, KMUL,
-                      bshift);
-        prevRecvH = recvH;
-        recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
-        recvF = (uint32_t)shr_lane((int32_t)f);
-        T = tnext;
-        tnext = tcol[c + 2 + G];
-        wf16f_step<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, qs, HB, HA, Ek, key, f, KK, OEK, EXT, BB,
-                      KMUL, bshift);
-        prevRecvH = recvH;
-        recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
-        recvF = (uint32_t)shr_lane((int32_t)f);
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KK);
+        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), NN);
+        f = pk_max3(toe, pk_subnb(f, EXT), NN);
+        diag = Hin[k];
+        Hout[k] = H;
     }
+    f_out = f;
 }
 
-template <int G, int R>
-__global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_local_kernel(WfArgs A) {
+// ---------------------------------------------------------------------------
+// SEMI step (transposed): registers = target columns, one query row per step.
+// Stored values are H - OE ("Hm").  In: diag_top = Hm(r-1, c0-1),
+// hl/el = Hm(r, c0-1) / E(r, c0-1) entering the lane's first column.
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top, uint32_t &hl, uint32_t &el,
+                                          const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
+                                          uint32_t (&Fk)[R], const uint32_t OE, const uint32_t EXT) {
+    uint32_t diag = diag_top, h = hl, e = el;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t tmp = pk_addnc(diag, v);                     // H(r-1,c-1) + s
+        Fk[k] = pk_max_u16(Hin[k], pk_subnb(Fk[k], EXT));            // F(r,c)
+        e = pk_max_u16(h, pk_subnb(e, EXT));                         // E(r,c)
+        h = pk_subnb(pk_max3(tmp, Fk[k], e), OE);                    // H(r,c) - OE
+        diag = Hin[k];
+        Hout[k] = h;
+    }
+    hl = h;
+    el = e;
+}
+
+// ---------------------------------------------------------------------------
+// The kernel.
+// ---------------------------------------------------------------------------
+template <int ALGO, int G, int R>
+__global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int S = 64 / G;            // lane groups per wave
+    constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1), slot = lane / G;
     const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * (2 * S);
-    uint32_t pr[2], ql[2], tl[2], qo[2], to[2], qpad[2], tpad[2];
+    uint32_t pr[2], xl[2], yl[2], xo[2], yo[2], xpad[2], ypad[2];
     bool valid[2];
+    const uint8_t *X = TR ? A.t : A.q, *Y = TR ? A.q : A.t;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         pr[h] = pair0 + 2 * slot + h;
         valid[h] = pr[h] < A.n;
-        ql[h] = valid[h] ? A.qlen[pr[h]] : 0;
-        tl[h] = valid[h] ? A.tlen[pr[h]] : 0;
-        qo[h] = valid[h] ? A.qoff[pr[h]] : 0;
-        to[h] = valid[h] ? A.toff[pr[h]] : 0;
-        qpad[h] = (ql[h] + 7u) & ~7u;
-        tpad[h] = (tl[h] + 7u) & ~7u;
+        const uint32_t ql = valid[h] ? A.qlen[pr[h]] : 0, tl = valid[h] ? A.tlen[pr[h]] : 0;
+        const uint32_t qo = valid[h] ? A.qoff[pr[h]] : 0, to = valid[h] ? A.toff[pr[h]] : 0;
+        xl[h] = TR ? tl : ql; yl[h] = TR ? ql : tl;
+        xo[h] = TR ? to : qo; yo[h] = TR ? qo : to;
+        xpad[h] = (xl[h] + 7u) & ~7u;
+        ypad[h] = (yl[h] + 7u) & ~7u;
     }
-    uint32_t tmaxw = max(tpad[0], tpad[1]);
+    uint32_t ymaxw = max(ypad[0], ypad[1]);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) tmaxw = max(tmaxw, (uint32_t)__shfl_xor(tmaxw, m));
-    // ---- stage both pairs' target codes, one uint2 per column (.y = lo: pair 0 code,
-    //      hi: pair 1 code; .x = later the fast path's T0), columns [-G, tmaxw + G)
-    //      so that out-of-range steps read "outside" ----
-    const uint32_t words = A.lds_stride >> 3;            // columns per slot, >= tmaxw + 2G + 4, multiple of 4
+    for (int m = 32; m >= 1; m >>= 1) ymaxw = max(ymaxw, (uint32_t)__shfl_xor(ymaxw, m));
+
+    const Pk16 P = pk16_params<ALGO>(A);
+    const int32_t NS = A.has_npen ? -A.npen : 0;
+    // table bytes for a Y code (per X letter j): match / mismatch / N / outside
+    const int32_t nrule = (ALGO == WF_GLOBAL) ? (A.has_npen ? NS : -A.b) : NS;   // gasal_kernels.h:44-54
+    const uint32_t t_mis = (uint32_t)(P.k - A.b) * 0x01010101u;
+    const uint32_t t_n = (uint32_t)(nrule + P.k) * 0x01010101u;
+    const uint32_t t_out = (uint32_t)P.k * 0x01010101u;            // score 0
+    const uint32_t t_match = (uint32_t)(A.a + P.k);
+
+    // ---- stage the step-axis sequences as score tables, one uint2 per position
+    //      (x: pair 0, y: pair 1), positions [-G, ymaxw + G) ----
+    const uint32_t words = A.lds_stride >> 3;            // positions per slot, >= ymaxw + 2G + 4, multiple of 4
     uint2 *wl = reinterpret_cast<uint2 *>(lds) + (size_t)wave * S * words;
-    bool other = false;                                  // a code the fast path cannot score
+    bool other = false;                                  // a code the packed path cannot score
     for (uint32_t base = 0; base < S * (words >> 2); base += 64) {
         const uint32_t idx = base + lane;
         const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
-        const uint32_t c0 = 4 * (idx - ps * (words >> 2)) - G;   // first column of this quad
-        uint32_t v[2];
+        const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;   // first position of this quad
+        uint32_t tab[2][4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const uint32_t tp = __shfl(tpad[h], ps * G), tof = __shfl(to[h], ps * G);
-            v[h] = 0xFFFFFFFFu;
-            if ((int32_t)c0 >= 0 && c0 < tp) {
-                v[h] = load4_codes(A.t, tof, c0 >> 2, A.packed);
+            const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
+            uint32_t v = 0;
+            const bool in = (int32_t)y0 >= 0 && y0 < yp;
+            if (in) v = load4_codes(Y, yof, y0 >> 2, A.packed);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) other |= letter_of((v[h] >> (8 * j)) & 15u, A.nval) == 5;
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t l = in ? letter_of((v >> (8 * j)) & 15u, A.nval) : 6u;
+                other |= l == 5;
+                tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
             }
         }
         if (idx < S * (words >> 2)) {
             uint2 *dst = wl + ps * words + 4 * (idx - ps * (words >> 2));
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                dst[j] = make_uint2(0u, ((v[0] >> (8 * j)) & 0xFFu) | (((v[1] >> (8 * j)) & 0xFFu) << 16));
+            for (int j = 0; j < 4; ++j) dst[j] = make_uint2(tab[0][j], tab[1][j]);
         }
     }
-    // ---- query codes: letter per row and pair, N / foreign-code census ----
+    // ---- register-axis letters: selector bytes 0 / 2 (0x0C = constant 0 outside) ----
     const uint32_t r0 = lg * R;
-    bool has_n = false;
-    uint32_t qs[R];
+    uint32_t xs[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t r = r0 + k;
-        qs[k] = 0x0C000C00u | 0x000C000Cu;    // selector "constant 0" for rows outside the query
+        xs[k] = 0x0C0C0C0Cu;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            if (valid[h] && r < qpad[h]) {
-                const uint32_t cde = A.packed ? (load4_codes(A.q, qo[h], r >> 2, 1) >> (8 * (r & 3))) & 15u
-                                              : (uint32_t)A.q[qo[h] + r] & 15u;
+            if (valid[h] && r < xpad[h]) {
+                const uint32_t cde = A.packed ? (load4_codes(X, xo[h], r >> 2, 1) >> (8 * (r & 3))) & 15u
+                                              : (uint32_t)X[xo[h] + r] & 15u;
                 const uint32_t l = letter_of(cde, A.nval);
-                has_n |= l == 4 && r < ql[h];
-                other |= l == 5 || (l == 4) != (r >= ql[h]);   // pad rows must be N (fast path scores them -K)
-                if (l < 4) qs[k] = (qs[k] & ~(0xFFu << (16 * h))) | ((l + 4 * h) << (16 * h));
+                if (r < xl[h]) {
+                    other |= l >= 4;                 // real positions must be A/C/G/T
+                    xs[k] = (xs[k] & ~(0xFFu << (16 * h))) | ((l + 4 * h) << (16 * h));
+                } else if (ALGO == WF_LOCAL) {
+                    other |= l != 4;                 // LOCAL pads must be N (scored -K here, dominated)
+                }
             }
         }
     }
     const bool fast = A.fast16 && !A.force_exact && !__syncthreads_or(other);
-    const uint32_t nsteps = tmaxw + G - 1;
-    const uint2 *tcol = wl + slot * words;
-    uint32_t key[R];
-    if (fast) {
-        // codes -> per-column score tables (byte j = score(letter j, t) + Kt; Kt outside the grid)
-        const int32_t K = fast16_params(A).k;
-        const int32_t NS = A.has_npen ? -A.npen : 0;
-        const uint32_t mis = (uint32_t)(K - A.b) * 0x01010101u, nrow = (uint32_t)(NS + K) * 0x01010101u;
-        const uint32_t outside = (uint32_t)K * 0x01010101u;
-        for (uint32_t e = lane; e < S * words; e += 64) {
-            const uint32_t cw = wl[e].y;
-            uint32_t tab[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t t = (cw >> (16 * h)) & 0xFFu;
-                const uint32_t l = t == 0xFFu ? 6u : letter_of(t, A.nval);
-                tab[h] = l == 6 ? outside : l == 4 ? nrow
-                                                   : (mis & ~(0xFFu << (8 * l))) | ((uint32_t)(A.a + K) << (8 * l));
-            }
-            wl[e] = make_uint2(tab[0], tab[1]);
-        }
-        __syncthreads();
-        wf16f_body<G, R>(A, tcol, lg, nsteps, qs, key);
-    } else {
-        // general path: nibble codes, row k's nibble at bit 8 + 4*(k&1) of each half
-        uint32_t qp[(R + 1) / 2];
-#pragma unroll
-        for (int j = 0; j < (R + 1) / 2; ++j) qp[j] = 0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint32_t r = r0 + k;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                uint32_t cde = 0;
-                if (valid[h] && r < qpad[h])
-                    cde = A.packed ? (load4_codes(A.q, qo[h], r >> 2, 1) >> (8 * (r & 3))) & 15u
-                                   : (uint32_t)A.q[qo[h] + r] & 15u;
-                qp[k >> 1] |= cde << (8 + 4 * (k & 1) + 16 * h);
-            }
-        }
-        const bool npen = A.has_npen && A.npen != 0;
-        const bool exact = A.force_exact || __any(has_n);
-        if (npen) {
-            if (exact) wf16_body<G, R, true, true>(A, tcol, lg, nsteps, qp, key);
-            else wf16_body<G, R, true, false>(A, tcol, lg, nsteps, qp, key);
-        } else {
-            if (exact) wf16_body<G, R, false, true>(A, tcol, lg, nsteps, qp, key);
-            else wf16_body<G, R, false, false>(A, tcol, lg, nsteps, qp, key);
-        }
-    }
+    if (threadIdx.x == 0) A.handled[blockIdx.x] = fast ? 1 : 0;
+    if (!fast) return;                                   // the int32 kernel takes this block
 
-    // ---- strip-major first maximum per pair (Q1) ----
+    const uint32_t nsteps = ymaxw + G - 1;
+    const uint2 *tcol = wl + slot * words;
+    const uint32_t OE = pk_bcast(A.o + A.e);
+    const uint32_t EXT = pk_bcast(A.e);
+    const uint32_t BB = (uint32_t)P.base * 0x10001u;
+    const uint32_t NN = (uint32_t)P.neg * 0x10001u;
+    const bool top = lg == 0;
+    int32_t c = -(int32_t)lg;                            // step-axis position of this lane
+
+    if (ALGO == WF_LOCAL) {
+        const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
+        const uint32_t KMUL = A.one << 8;
+        const uint32_t bshift = ((uint32_t)P.base << 8) & 0xFFFFu;
+        uint32_t HA[R], HB[R], Ek[R], key[R];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        uint64_t best = 0;
+        for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
+        uint32_t recvH = BB, prevRecvH = BB, recvF = BB, f = BB;
+        uint2 tnext = tcol[c + G];
+        for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
+            uint2 T = tnext;
+            tnext = tcol[c + 1 + G];
+            step_local<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, f, KK, OEK, EXT, BB,
+                          KMUL, bshift);
+            prevRecvH = recvH;
+            recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
+            recvF = (uint32_t)shr_lane((int32_t)f);
+            T = tnext;
+            tnext = tcol[c + 2 + G];
+            step_local<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, f, KK, OEK, EXT,
+                          BB, KMUL, bshift);
+            prevRecvH = recvH;
+            recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
+            recvF = (uint32_t)shr_lane((int32_t)f);
+        }
+        // ---- strip-major first maximum per pair (Q1) ----
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint32_t r = r0 + k;
-            const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
-            const uint32_t H = kk >> 8;
-            if (r < qpad[h] && H > 0) {
-                const uint32_t col = 255u - (kk & 0xFFu);
-                const uint32_t ord = (((col >> 3) * qpad[h] + r) << 3) + (col & 7);
-                const uint64_t cand = ((uint64_t)H << 32) | (0xFFFFFFFFu - ord);
-                best = cand > best ? cand : best;
+        for (int h = 0; h < 2; ++h) {
+            uint64_t best = 0;
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const uint32_t r = r0 + k;
+                const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
+                const uint32_t H = kk >> 8;
+                if (r < xpad[h] && H > 0) {
+                    const uint32_t col = 255u - (kk & 0xFFu);
+                    const uint32_t ord = (((col >> 3) * xpad[h] + r) << 3) + (col & 7);
+                    const uint64_t cand = ((uint64_t)H << 32) | (0xFFFFFFFFu - ord);
+                    best = cand > best ? cand : best;
+                }
+            }
+            best = group_max_u64<G>(best);
+            if (valid[h] && lg == 0) {
+                int32_t H = (int32_t)(best >> 32), qe = 0, te = 0;
+                if (H > 0) {
+                    const uint32_t ord = 0xFFFFFFFFu - (uint32_t)best;
+                    const uint32_t rest = ord >> 3;
+                    qe = (int32_t)(rest % xpad[h]);
+                    te = (int32_t)((rest / xpad[h]) * 8 + (ord & 7));
+                }
+                A.score[pr[h]] = H;                                   // local :428-430
+                if (A.qend) A.qend[pr[h]] = qe;
+                if (A.tend) A.tend[pr[h]] = te;
             }
         }
-        best = group_max_u64<G>(best);
-        if (valid[h] && lg == 0) {
-            int32_t H = (int32_t)(best >> 32), qe = 0, te = 0;
-            if (H > 0) {
-                const uint32_t ord = 0xFFFFFFFFu - (uint32_t)best;
-                const uint32_t rest = ord >> 3;
-                qe = (int32_t)(rest % qpad[h]);
-                te = (int32_t)((rest / qpad[h]) * 8 + (ord & 7));
+    } else if (ALGO == WF_GLOBAL) {
+        // boundaries (global.h:57-71, Q2): H(r,-1) = -(o+e*r) (0 for r = 0), E = -inf;
+        // top: H(-1,c-1) = -(o+e*c) (0 for c = 0), F = -inf.  Lanes sweep garbage
+        // columns c < -1 first and reset to the left boundary at c = -1.
+        const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
+        const int32_t pb = P.base, go = A.o, ge = A.e;
+        auto left = [=](int32_t r) -> uint32_t { return (uint32_t)(pb - (r <= 0 ? 0 : go + ge * r)) * 0x10001u; };
+        uint32_t HA[R], HB[R], Ek[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) { HA[k] = left((int32_t)(r0 + k)); HB[k] = HA[k]; Ek[k] = NN; }
+        uint32_t recvH = left((int32_t)r0 - 1), prevRecvH = recvH, recvF = NN, f = NN;
+        uint32_t kq_lane[2], kq[2];
+        int32_t score[2] = {0, 0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            kq_lane[h] = (xl[h] - 1) / R;
+            kq[h] = (xl[h] - 1) - kq_lane[h] * R;
+        }
+        uint2 tnext = tcol[c + G];
+        auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+            const uint2 T = tnext;
+            tnext = tcol[cc + 1 + G];
+            if (cc == -1) {
+                int32_t rr = (int32_t)r0;
+                asm volatile("" : "+v"(rr));   // keep the R boundary values out of loop-invariant registers
+#pragma unroll
+                for (int k = 0; k < R; ++k) { Hout[k] = left(rr + k); Ek[k] = NN; }
+                f = NN;
+            } else {
+                const uint32_t dtop = (uint32_t)(pb - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
+                step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KK, OEK, EXT, NN);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int k = 0; k < R; ++k) v = (k == (int)kq[h]) ? Hout[k] : v;
+                        score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb;
+                    }
+                }
             }
-            A.score[pr[h]] = H;
-            if (A.qend) A.qend[pr[h]] = qe;
-            if (A.tend) A.tend[pr[h]] = te;
+            prevRecvH = recvH;
+            recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
+            recvF = (uint32_t)shr_lane((int32_t)f);
+        };
+        for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
+            half_step(c, HA, HB);
+            half_step(c + 1, HB, HA);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (valid[h] && lg == kq_lane[h]) A.score[pr[h]] = score[h];
+    } else {
+        // SEMI, transposed: c is the query row of this step, registers are the
+        // target columns lg*R + k.  Boundaries (semiglobal_kernel_template.h):
+        //   left  H(r,-1) = head_q ? 0 : -(o+e*r) (0 for r = 0); E(r,-1) = head_q ? 0 : -inf  (:87-99, Q2)
+        //   top   diag into (0,c): head_t ? 0 : -(o+e*c) (0 for c = 0)                         (:127)
+        //         F(0,c) = hu(c) - OE, hu(c) = head_t ? 0 : -(o+e*c)                           (:125, Q3)
+        // Lanes sweep garbage rows r < -1 first and reset to row -1 at r = -1.
+        const bool head_q = (A.head == 1 || A.head == 3), head_t = (A.head == 2 || A.head == 3);
+        const int32_t oe = A.o + A.e, pb = P.base, go = A.o, ge = A.e;
+        auto hm = [=](int32_t val) -> uint32_t { return (uint32_t)(pb + val - oe) * 0x10001u; };   // H - OE
+        auto hleft = [=](int32_t r) -> uint32_t {      // Hm(r, -1); r = -1 gives H(-1,-1) = 0
+            return (uint32_t)(pb - oe + (head_q ? 0 : (r <= 0 ? 0 : -(go + ge * r)))) * 0x10001u;
+        };
+        const uint32_t eleft = head_q ? BB : NN;        // E(r,-1)
+        uint32_t HA[R], HB[R], Fk[R];
+        auto reset = [&](uint32_t (&H)[R]) {
+            // computed where used: hoisting 2R loop-invariant values out of the sweep would spill
+            int32_t c0 = (int32_t)r0;
+            asm volatile("" : "+v"(c0));
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const int32_t col = c0 + k;
+                const int32_t hd = head_t ? 0 : -(go + ge * (col + 1));   // H(-1,col) as diag of (0,col+1)
+                const int32_t hu = head_t ? 0 : -(go + ge * col);         // H(-1,col) as F source (Q3)
+                H[k] = hm(hd);
+                Fk[k] = (uint32_t)(pb + hu - oe + ge) * 0x10001u;         // F(0,col) = hu - OE exactly
+            }
+        };
+        reset(HA);
+#pragma unroll
+        for (int k = 0; k < R; ++k) HB[k] = HA[k];
+        // TAIL=TARGET: max over the last query row, columns < tl, first (smallest) column
+        uint32_t best[2] = {0, 0};
+        uint32_t recvH = HA[R - 1], prevRecvH = HA[R - 1], recvE = NN, hl = 0, el = 0;
+        uint2 tnext = tcol[c + G];
+        auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+            const uint2 T = tnext;
+            tnext = tcol[cc + 1 + G];
+            if (cc == -1) {
+                reset(Hout);
+            } else {
+                hl = top ? hleft(cc) : recvH;
+                el = top ? eleft : recvE;
+                step_semi<R>(T, top ? hleft(cc - 1) : prevRecvH, hl, el, xs, Hin, Hout, Fk, OE, EXT);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (valid[h] && cc == (int32_t)yl[h] - 1) {                 // semiglobal :160-178
+#pragma unroll
+                        for (int k = 0; k < R; ++k) {
+                            const uint32_t col = r0 + k;
+                            const uint32_t v = (Hout[k] >> (16 * h)) & 0xFFFFu;
+                            const uint32_t cand = col < xl[h] ? (v << 16) | (0xFFFFu - col) : 0u;
+                            best[h] = cand > best[h] ? cand : best[h];
+                        }
+                    }
+                }
+            }
+            prevRecvH = recvH;
+            recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
+            recvE = (uint32_t)shr_lane((int32_t)el);
+        };
+        for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
+            half_step(c, HA, HB);
+            half_step(c + 1, HB, HA);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t b = best[h];
+#pragma unroll
+            for (int m = 1; m < G; m <<= 1) b = max(b, (uint32_t)__shfl_xor(b, m));
+            if (valid[h] && lg == 0) {
+                // semiglobal :49,63-64,206-218 (Q10): q_end = tl, t_end = column of the max
+                int32_t score = -32768, qe = (int32_t)xl[h], te = (int32_t)yl[h];
+                if (b != 0) {
+                    score = (int32_t)(b >> 16) - pb + oe;
+                    te = (int32_t)(0xFFFFu - (b & 0xFFFFu));
+                }
+                A.score[pr[h]] = score;
+                if (A.qend) A.qend[pr[h]] = qe;
+                if (A.tend) A.tend[pr[h]] = te;
+            }
         }
     }
 }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes for one bench workload (separate rocprofv3 runs; --pmc never combined with
 # runtime/sys traces).  Usage: pmc_session.sh TAG [bench args...]
+# Summarise afterwards (on the host): python tools/pmc_summary.py gpurun_out/pmc_TAG WORKLOAD PAIRS
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=${1:-r01}; shift || true
@@ -8,7 +9,6 @@ OUT="$ROOT/gpurun_out/pmc_$TAG"
 mkdir -p "$OUT"
 fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > "$OUT/avail.txt" 2>&1; echo "list rc=$?"
 i=0
 for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
             "FETCH_SIZE" "WRITE_SIZE" \

@@ -217,7 +217,43 @@ def test_packed_input(engine):
 def test_plan_is_wavefront_for_bench_configs():
     assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150).startswith("wavefront16_local")
     assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300).startswith("wavefront_global_tb")
-    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL), 150, 182).startswith("wavefront_semi")
+    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL), 150, 182).startswith("wavefront16_semi")
+    assert G.describe_plan(G.make_params(algo=G.GLOBAL), 300, 300).startswith("wavefront16_global")
+
+
+# ------------------------------------------ packed kernels + int32 fallback ----
+@pytest.mark.parametrize("algo,kw", [(G.GLOBAL, {}), (G.SEMI_GLOBAL, dict(head=G.TARGET, tail=G.TARGET)),
+                                     (G.SEMI_GLOBAL, dict(head=G.NONE, tail=G.TARGET)),
+                                     (G.SEMI_GLOBAL, dict(head=G.QUERY, tail=G.TARGET)),
+                                     (G.LOCAL, {})])
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTN", b"ACGTACGTACGTACGTN", b"ACGTRYacgt"])
+def test_packed_paths_with_declined_blocks(engine, algo, kw, alphabet):
+    # blocks holding a code the packed kernel cannot score are re-aligned by the int32 kernel
+    rng = np.random.default_rng(hash((algo, alphabet)) & 0xFFFF)
+    qs, ts = helpers.random_pairs(rng, 1500, 1, 180, 1, 200, alphabet=alphabet)
+    b = G.Batch.from_pairs(qs, ts)
+    check(engine, b, algo=algo, **kw)
+
+
+@pytest.mark.parametrize("n", [1, 2, 31, 65, 333])
+@pytest.mark.parametrize("algo", [G.GLOBAL, G.SEMI_GLOBAL])
+def test_packed_odd_batch_sizes(engine, n, algo):
+    b = rand_batch(200 + n, n, 1, 190, 1, 190)
+    check(engine, b, algo=algo, head=G.TARGET, tail=G.TARGET)
+
+
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2), (5, 4, 10, 1), (1, 1, 0, 1), (3, 6, 0, 0)])
+@pytest.mark.parametrize("algo", [G.GLOBAL, G.SEMI_GLOBAL])
+def test_packed_scores(engine, scores, algo):
+    a, bb, o, e = scores
+    b = rand_batch(300 + a * 7 + bb, 500, 30, 160, 30, 190)
+    check(engine, b, algo=algo, head=G.TARGET, tail=G.TARGET, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+
+
+@pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL, G.SEMI_GLOBAL])
+def test_packed_with_n_penalty(engine, algo):
+    b = rand_batch(400 + algo, 800, 20, 150, 20, 180, alphabet=b"ACGTACGTN")
+    check(engine, b, algo=algo, head=G.TARGET, tail=G.TARGET, n_penalty=2)
 
 
 def test_config2_sample_exact(engine):

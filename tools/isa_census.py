@@ -22,12 +22,14 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 # plan name (gasalx_describe_plan) -> (kernel symbol, rows per lane R, group G, pairs per lane)
 PLANS = {
-    "wavefront16_local_G8R19": ("_ZN2gx17wf16_local_kernelILi8ELi19EEEvNS_6WfArgsE", 19, 8, 2),
-    "wavefront16_local_G8R20": ("_ZN2gx17wf16_local_kernelILi8ELi20EEEvNS_6WfArgsE", 20, 8, 2),
-    "wavefront_local_keys_G8R20": ("_ZN2gx9wf_kernelILi0ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1),
-    "wavefront_global_tb_G16R20": ("_ZN2gx9wf_kernelILi1ELb0ELb1ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 1),
-    "wavefront_semi_keys_G8R20": ("_ZN2gx9wf_kernelILi2ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1),
-    "wavefront_semi_G8R20": ("_ZN2gx9wf_kernelILi2ELb0ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1),
+    # plan name: (kernel symbol, R, G, pairs per lane, step axis)
+    "wavefront16_local_G8R19": ("_ZN2gx11wf16_kernelILi0ELi8ELi19EEEvNS_6WfArgsE", 19, 8, 2, "target"),
+    "wavefront16_local_G8R20": ("_ZN2gx11wf16_kernelILi0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 2, "target"),
+    "wavefront16_global_G16R20": ("_ZN2gx11wf16_kernelILi1ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 2, "target"),
+    "wavefront16_semi_G8R23": ("_ZN2gx11wf16_kernelILi2ELi8ELi23EEEvNS_6WfArgsE", 23, 8, 2, "query"),
+    "wavefront_local_keys_G8R20": ("_ZN2gx9wf_kernelILi0ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1, "target"),
+    "wavefront_global_tb_G16R20": ("_ZN2gx9wf_kernelILi1ELb0ELb1ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 1, "target"),
+    "wavefront_semi_keys_G8R20": ("_ZN2gx9wf_kernelILi2ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1, "target"),
 }
 
 
@@ -61,7 +63,7 @@ def main():
                         "-o", asm], check=True)
     lines = open(asm).read().split("\n")
     out = {}
-    for plan, (sym, R, Gs, ppl) in PLANS.items():
+    for plan, (sym, R, Gs, ppl, axis) in PLANS.items():
         # the column-step loop: DPP hand-offs and at least ~5 VALU per row
         cands = [l for l in loops(lines, sym) if l["dpp"] >= 2 and l["dpp"] % 2 == 0
                  and l["valu"] / (l["dpp"] // 2) >= 5 * R]
@@ -69,7 +71,7 @@ def main():
             continue
         best = min(cands, key=lambda l: l["valu"] / (l["dpp"] // 2))
         steps = best["dpp"] // 2
-        out[plan] = dict(kernel=sym, R=R, G=Gs, pairs_per_lane=ppl, steps_per_iteration=steps,
+        out[plan] = dict(kernel=sym, R=R, G=Gs, pairs_per_lane=ppl, step_axis=axis, steps_per_iteration=steps,
                          valu_per_step=best["valu"] / steps, s_nop_per_step=best["s_nop"] / steps,
                          valu_per_padded_cell=best["valu"] / steps / (64 * R * ppl))
     path = os.path.join(ROOT, "profiles", "isa_census.json")

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/pmc_session.sh run into profiles/pmc_<workload>.json.
+
+usage: pmc_summary.py RUN_DIR WORKLOAD PAIRS_PER_LAUNCH
+For the dominant kernel of the bench step (the longest dispatch of the last
+bench step), records every counter of every pass and the derived:
+  hbm_bytes_per_launch   = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes; gfx950
+                           FETCH_SIZE tallies 128-B requests at 64 B, see
+                           MI355X_MICROARCH.md, HBM section)
+  valu_insts_per_launch  = SQ_INSTS_VALU (wave instructions)
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(run_dir, workload, pairs):
+    per = collections.defaultdict(dict)   # kernel -> counter -> value (last dispatch of that kernel)
+    dur = {}
+    for path in sorted(glob.glob(os.path.join(run_dir, "p*", "run_counter_collection.csv"))):
+        rows = list(csv.DictReader(open(path)))
+        agg = collections.defaultdict(float)
+        last = {}
+        for r in rows:
+            k = r["Kernel_Name"]
+            d = int(r["Dispatch_Id"])
+            agg[(k, d, r["Counter_Name"])] += float(r["Counter_Value"])
+            last[k] = max(last.get(k, -1), d)
+            dur[(k, d)] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        for (k, d, c), v in agg.items():
+            if d == last[k]:
+                per[k][c] = v
+    # dominant kernel: longest last dispatch
+    best = max(per, key=lambda k: max(v for (kk, _), v in dur.items() if kk == k))
+    c = per[best]
+    out = {"workload": workload, "kernel": best, "pairs_per_launch": int(pairs), "counters": c}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        out["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
+    if "SQ_INSTS_VALU" in c:
+        out["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    out["note"] = ("separate rocprofv3 --pmc passes (scripts/pmc_session.sh); FETCH_SIZE x2 per the gfx950 "
+                   "correction; counters of the last dispatch of the dominant kernel")
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    json.dump(out, open(path, "w"), indent=1, sort_keys=True)
+    print(path, {k: out[k] for k in out if k not in ("counters", "note")})
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3])
