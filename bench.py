@@ -9,7 +9,7 @@ torch's current stream.  Multi-GPU: one process per GPU, each aligns its own
 batch (weak scaling, no data-path collective); timing is bracketed by a
 barrier + synchronize and the max over ranks is reported.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--workload sw_local|nw_tb|semi]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--workload sw_local|nw_tb|semi|pairhmm]
 """
 import argparse
 import json
@@ -38,7 +38,54 @@ WORKLOADS = {
               "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
     "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
              "config4 shard: semi-global TARGET/TARGET, 150bp reads in 182bp windows, seed 0x5EED0004"),
+    "pairhmm": (5, 100_000, None, 4762, 11,
+                "config5: PairHMM fp32 forward, 100K reads x haplotypes (250 x 500), seed 0x5EED0005"),
 }
+METRICS = {
+    "pairhmm": "GCUPS of PairHMM fp32 forward (config 5, 250x500) on MI355X",
+}
+
+
+def synth_pairhmm(n, seed, rl=250, hl=500):
+    """haplotype 500 bp uniform; read = 250-bp substring with
+    2% mismatches; base quals U[10,40], insertion/deletion quals 45 (gcp ignored)."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"ACGT", np.uint8)
+    haps = alpha[rng.integers(0, 4, (n, hl))]
+    start = rng.integers(0, hl - rl + 1, n)
+    reads = haps[np.arange(n)[:, None], start[:, None] + np.arange(rl)[None, :]].copy()
+    flip = rng.random((n, rl)) < 0.02
+    reads[flip] = alpha[(np.searchsorted(alpha, reads[flip]) + rng.integers(1, 4, int(flip.sum()))) % 4]
+    bq = rng.integers(10, 41, n * rl).astype(np.uint8)
+    iq = np.full(n * rl, 45, np.uint8)
+    qm, de, xi, al = G.pairhmm_params(bq, iq, iq)
+    return dict(reads=reads.reshape(-1), read_offsets=np.arange(n, dtype=np.uint32) * rl,
+                read_lens=np.full(n, rl, np.uint32), qm=qm, delta=de, xiksi=xi, alpha=al, haps=haps.reshape(-1),
+                hap_offsets=np.arange(n, dtype=np.uint32) * hl, hap_lens=np.full(n, hl, np.uint32))
+
+
+def cpu_baseline_pairhmm(h, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    n = len(h["read_lens"])
+    chunk, done, cells, t_used = 2000, 0, 0, 0.0
+    while t_used < budget_s and done < n:
+        e = min(done + chunk, n)
+        rl, hl = h["read_lens"][done:e], h["hap_lens"][done:e]
+        r0, h0 = int(h["read_offsets"][done]), int(h["hap_offsets"][done])
+        r1, h1 = int(h["read_offsets"][e - 1] + rl[-1]), int(h["hap_offsets"][e - 1] + hl[-1])
+        t0 = time.perf_counter()
+        O.pairhmm(h["reads"][r0:r1], h["read_offsets"][done:e] - r0, rl, h["qm"][r0:r1], h["delta"][r0:r1],
+                  h["xiksi"][r0:r1], h["alpha"][r0:r1], h["haps"][h0:h1], h["hap_offsets"][done:e] - h0, hl,
+                  n_threads=threads)
+        t_used += time.perf_counter() - t0
+        cells += int(np.sum(rl.astype(np.int64) * hl.astype(np.int64)))
+        done = e
+    return {"value": round(cells / t_used / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+            "sample": f"first {done} pairs of the rank-0 batch ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
+                      f"oracle/gasal_oracle.c orc_pairhmm_batch OpenMP x{threads}"}
 
 
 def parse():
@@ -91,37 +138,52 @@ def main():
 
     kind, default_pairs, pkw, bytes_per_pair, ops_per_cell, label = WORKLOADS[args.workload]
     n = args.pairs or default_pairs
-    seed = {2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004}[kind] + rank
-    batch = G.Batch.synth(kind, n, seed)
-    cells_per_step = int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
-    params = G.make_params(**pkw)
-
-    # inputs resident in HBM before the timed region
-    as_i32 = lambda a: torch.from_numpy(a.view(np.int32).copy()).to(dev)
-    d = {
-        "q_batch": torch.from_numpy(batch.q_data).to(dev), "t_batch": torch.from_numpy(batch.t_data).to(dev),
-        "q_offsets": as_i32(batch.q_offsets), "t_offsets": as_i32(batch.t_offsets),
-        "q_lens": as_i32(batch.q_lens), "t_lens": as_i32(batch.t_lens),
-        "aln_score": torch.empty(n, dtype=torch.int32, device=dev),
-    }
-    if pkw["algo"] != G.GLOBAL:
-        d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
-        d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
-    if pkw.get("start_pos") == G.WITH_TB:
-        d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
-        d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)
-    ptrs = {k: v.data_ptr() for k, v in d.items()}
+    seed = {2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005}[kind] + rank
     eng = G.Engine(local_rank)
     stream = torch.cuda.Stream(dev)      # a real (non-null) stream: kernels and timing events share it
     torch.cuda.set_stream(stream)
-    maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
+    gathered = None
+    if kind == 5:
+        h = synth_pairhmm(n, seed)
+        cells_per_step = int(np.sum(h["read_lens"].astype(np.int64) * h["hap_lens"].astype(np.int64)))
+        dh = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32 else v).to(dev)
+              for k, v in h.items()}
+        result = torch.empty(n, dtype=torch.float32, device=dev)
+        hptrs = {k: v.data_ptr() for k, v in dh.items()}
+        maxr, maxh = int(h["read_lens"].max()), int(h["hap_lens"].max())
+        plan = f"pairhmm_wavefront (read {maxr} x hap {maxh})"
 
-    gathered = [torch.empty_like(d["aln_score"]) for _ in range(world)] if (args.gather and world > 1) else None
+        def step():
+            eng.pairhmm_device_ptrs(hptrs, len(h["reads"]), len(h["haps"]), n, maxr, maxh, result.data_ptr(),
+                                    stream.cuda_stream)
+    else:
+        batch = G.Batch.synth(kind, n, seed)
+        cells_per_step = int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
+        params = G.make_params(**pkw)
 
-    def step():
-        eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, maxq, maxt, stream.cuda_stream)
-        if gathered is not None:   # optional exchange step of SURVEY §8(e): every rank gets all scores
-            dist.all_gather(gathered, d["aln_score"])
+        # inputs resident in HBM before the timed region
+        as_i32 = lambda a: torch.from_numpy(a.view(np.int32).copy()).to(dev)
+        d = {
+            "q_batch": torch.from_numpy(batch.q_data).to(dev), "t_batch": torch.from_numpy(batch.t_data).to(dev),
+            "q_offsets": as_i32(batch.q_offsets), "t_offsets": as_i32(batch.t_offsets),
+            "q_lens": as_i32(batch.q_lens), "t_lens": as_i32(batch.t_lens),
+            "aln_score": torch.empty(n, dtype=torch.int32, device=dev),
+        }
+        if pkw["algo"] != G.GLOBAL:
+            d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+            d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+        if pkw.get("start_pos") == G.WITH_TB:
+            d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
+            d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)
+        ptrs = {k: v.data_ptr() for k, v in d.items()}
+        maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
+        plan = G.describe_plan(params, maxq, maxt)
+        gathered = [torch.empty_like(d["aln_score"]) for _ in range(world)] if (args.gather and world > 1) else None
+
+        def step():
+            eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, maxq, maxt, stream.cuda_stream)
+            if gathered is not None:   # optional exchange step of SURVEY §8(e): every rank gets all scores
+                dist.all_gather(gathered, d["aln_score"])
 
     for _ in range(args.warmup):
         step()
@@ -151,7 +213,6 @@ def main():
         gcups = total_cells / elapsed / 1e9
         kern_s = kern_ms / 1e3
         achieved = bytes_per_pair * n / kern_s / 1e9
-        plan = G.describe_plan(params, maxq, maxt)
         valu_roof = None
         pmc = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -169,7 +230,7 @@ def main():
                          "valu_insts_per_launch": pmc["valu_insts_per_launch"],
                          "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU)"}
         out = {
-            "metric": "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %",
+            "metric": METRICS.get(args.workload, "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %"),
             "value": round(gcups, 2),
             "unit": "GCUPS",
             "n_gpus": world,
@@ -179,7 +240,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "fp32" if kind == 5 else "int32",
             "data": "synthetic (SURVEY.md 8(d) generator, std::mt19937_64), resident in HBM",
             "config": {"workload": label, "pairs_per_gpu": n, "cells_per_gpu_step": cells_per_step,
                        "plan": plan,
@@ -192,7 +253,8 @@ def main():
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(batch, pkw, args.cpu_seconds)
+            out["cpu_baseline"] = (cpu_baseline_pairhmm(h, args.cpu_seconds) if kind == 5
+                                   else cpu_baseline(batch, pkw, args.cpu_seconds))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

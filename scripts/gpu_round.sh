@@ -22,6 +22,7 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_sw_local 600 python bench.py
 step bench_nw_tb 600 python bench.py --workload nw_tb --no-cpu --steps 10
 step bench_semi 600 python bench.py --workload semi --no-cpu --steps 10
+step bench_pairhmm 600 python bench.py --workload pairhmm --steps 10 --cpu-seconds 8
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/prof_sw_local" -o run -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu > "$ROOT/$O/bench_prof.out" 2> "$ROOT/$O/bench_prof.err"
 echo "[rocprof] rc=$?"
