@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -71,9 +72,9 @@ static WfFn wf16_pick(int G, int R) {
     return nullptr;
 }
 
-static WfFn wf16_lookup(int algo, int G, int R) {
+static WfFn wf16_lookup(int algo, bool tb, int G, int R) {
     if (algo == WF_LOCAL) return wf16_pick<WF_LOCAL>(G, R);
-    if (algo == WF_GLOBAL) return wf16_pick<WF_GLOBAL>(G, R);
+    if (algo == WF_GLOBAL) return tb ? wf16_pick<WF16_GLOBAL_TB>(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return wf16_pick<WF_SEMI>(G, R);
 }
 
@@ -83,7 +84,9 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
 static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
-    if (p.second_best || p.start_pos != 0) return false;
+    if (p.second_best || p.start_pos == 1) return false;
+    if (p.start_pos == 2 && (wf_algo != WF_GLOBAL || !getenv("GASALX_PACKED_TB")))   // packed traceback: WIP
+        return false;
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
     const int64_t a = p.match, b = p.mismatch, oe = (int64_t)p.gap_open + p.gap_extend, e = p.gap_extend;
@@ -165,7 +168,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         }
         const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";
         if (pl.packed16)
-            pl.name = std::string("wavefront16_") + an + "_G" + std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
+            pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + "_G" + std::to_string(pl.G16) + "R" +
+                      std::to_string(pl.R16);
         else
             pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
                       std::to_string(pl.G) + "R" + std::to_string(pl.R);
@@ -283,7 +287,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             const uint32_t grid16 = grid_for(n, ppb16);
             HIPCHK(ws.misc.reserve(grid16 + 64));
             P16.handled = ws.misc.as<uint8_t>();
-            WfFn f16 = wf16_lookup(pl.wf_algo, pl.G16, pl.R16);
+            WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16);
             if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
             if (pl.lds16_bytes > 64 * 1024)
                 HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,

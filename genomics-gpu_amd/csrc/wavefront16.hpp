@@ -159,6 +159,58 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 }
 
 // ---------------------------------------------------------------------------
+// GLOBAL step with traceback nibbles (global.h:14-26): per cell
+//   low2 = (H == tmp) ? (s < 0) : ((H == F) ? 3 : 2);  bit2 = E extended;  bit3 = F extended
+// appended to dw (4 nibbles per 16-bit half; older ones fall off the top).
+// [x == 0] for x >= 0 is one saturating v_pk_sub_u16 (1 - x, clamped at 0).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {
+    return GX_AS(uint32_t, __builtin_elementwise_sub_sat(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
+}
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {   // modular per half
+    return GX_AS(uint32_t, GX_AS(pk_u2, a) - GX_AS(pk_u2, b));
+}
+
+template <int R>
+__device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
+                                               const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
+                                               uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
+                                               uint32_t &f_out, const uint32_t KK, const uint32_t OEK,
+                                               const uint32_t EXT, const uint32_t NN, const uint32_t ONE) {
+    const uint32_t TWO = ONE << 1;
+    uint32_t diag = diag_top, f = f_top;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KK);
+        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
+        const uint32_t En = pk_max3(toe, em, NN);
+        const uint32_t Fn = pk_max3(toe, fm, NN);
+        // direction nibble
+        const uint32_t z1 = pk_subsat_u16(ONE, pk_subnb(H, tmp));       // H came from the diagonal
+        const uint32_t z2 = pk_subsat_u16(ONE, pk_subnb(H, f));         // H == F
+        const uint32_t mx = pk_min_u16(pk_subsat_u16(KK, v), ONE);      // substitution score < 0
+        const uint32_t q = pk_addnc(z2, TWO);                            // 2 or 3
+        const uint32_t low = pk_mad_u16(z1, pk_sub16(mx, q), q);         // z1 ? mx : q
+        const uint32_t z4 = pk_subsat_u16(ONE, pk_subnb(En, em));       // E extended
+        const uint32_t z3 = pk_subsat_u16(ONE, pk_subnb(Fn, fm));       // F extended
+        const uint32_t nib = pk_mad_u16(z3, ONE << 3, pk_mad_u16(z4, ONE << 2, low));
+        dw[k] = pk_mad_u16(dw[k], ONE << 4, nib);
+        Ek[k] = En;
+        f = Fn;
+        diag = Hin[k];
+        Hout[k] = H;
+    }
+    f_out = f;
+}
+
+// ---------------------------------------------------------------------------
 // SEMI step (transposed): registers = target columns, one query row per step.
 // Stored values are H - OE ("Hm").  In: diag_top = Hm(r-1, c0-1),
 // hl/el = Hm(r, c0-1) / E(r, c0-1) entering the lane's first column.
@@ -185,9 +237,13 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 // ---------------------------------------------------------------------------
 // The kernel.
 // ---------------------------------------------------------------------------
-template <int ALGO, int G, int R>
-__global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
+constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
+
+template <int ALGO_, int G, int R>
+__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
+    constexpr int ALGO = GTB ? WF_GLOBAL : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -347,8 +403,11 @@ __global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
         const int32_t pb = P.base, go = A.o, ge = A.e;
         auto left = [=](int32_t r) -> uint32_t { return (uint32_t)(pb - (r <= 0 ? 0 : go + ge * r)) * 0x10001u; };
         uint32_t HA[R], HB[R], Ek[R];
+        uint32_t dw[GTB ? R : 1];                      // traceback nibbles: last 4 columns per half
 #pragma unroll
         for (int k = 0; k < R; ++k) { HA[k] = left((int32_t)(r0 + k)); HB[k] = HA[k]; Ek[k] = NN; }
+#pragma unroll
+        for (int k = 0; k < (GTB ? R : 1); ++k) dw[k] = 0;
         uint32_t recvH = left((int32_t)r0 - 1), prevRecvH = recvH, recvF = NN, f = NN;
         uint32_t kq_lane[2], kq[2];
         int32_t score[2] = {0, 0};
@@ -369,7 +428,29 @@ __global__ __launch_bounds__(kBlock, GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
                 f = NN;
             } else {
                 const uint32_t dtop = (uint32_t)(pb - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
-                step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KK, OEK, EXT, NN);
+                if constexpr (GTB) {
+                    step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, KK, OEK,
+                                      EXT, NN, A.one);
+                    if ((cc & 3) == 3 && cc >= 0) {
+                        // one word per (8-column strip, row), columns c..c+7 in nibbles 7..0 (global.h:170,262):
+                        // columns 0-3 of the strip are the word's high half, 4-7 its low half
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            if (valid[h] && (uint32_t)cc < ypad[h]) {
+                                uint16_t *dst = reinterpret_cast<uint16_t *>(
+                                                    A.tb + (uint64_t)pr[h] * A.tb_pair_words +
+                                                    (uint64_t)(cc >> 3) * xpad[h] + r0) +
+                                                ((cc & 4) ? 0 : 1);
+#pragma unroll
+                                for (int k = 0; k < R; ++k)
+                                    if (r0 + k < xpad[h]) dst[2 * k] = (uint16_t)(dw[k] >> (16 * h));
+                            }
+                        }
+                    }
+                } else {
+                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KK, OEK, EXT,
+                                   NN);
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299

@@ -334,3 +334,14 @@ def test_pairhmm_random_long(engine):
                           dq=np.full(R, 45)))
     args = _hmm_batch(pairs)
     np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
+
+
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2), (1, 1, 0, 1), (3, 6, 0, 0)])
+@pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTACGTACGTN", b"ACGTRY"])
+def test_packed_global_traceback(engine, scores, alphabet):
+    # packed traceback words (and the int32 kernel's for declined blocks) feed the same get_tb walk
+    a, bb, o, e = scores
+    rng = np.random.default_rng(hash((scores, alphabet)) & 0xFFFF)
+    qs, ts = helpers.random_pairs(rng, 700, 20, 310, 20, 310, alphabet=alphabet)
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+    check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)

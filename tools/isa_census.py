@@ -28,6 +28,7 @@ PLANS = {
     "wavefront16_global_G16R20": ("_ZN2gx11wf16_kernelILi1ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 2, "target"),
     "wavefront16_semi_G8R23": ("_ZN2gx11wf16_kernelILi2ELi8ELi23EEEvNS_6WfArgsE", 23, 8, 2, "query"),
     "wavefront_local_keys_G8R20": ("_ZN2gx9wf_kernelILi0ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1, "target"),
+    "wavefront16_global_tb_G16R20": ("_ZN2gx11wf16_kernelILi3ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 2, "target"),
     "wavefront_global_tb_G16R20": ("_ZN2gx9wf_kernelILi1ELb0ELb1ELi16ELi20EEEvNS_6WfArgsE", 20, 16, 1, "target"),
     "wavefront_semi_keys_G8R20": ("_ZN2gx9wf_kernelILi2ELb1ELb0ELi8ELi20EEEvNS_6WfArgsE", 20, 8, 1, "target"),
 }
