@@ -2,7 +2,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -34,7 +33,7 @@ void DevBuf::release() {
     bytes = 0;
 }
 void Workspace::release_all() {
-    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc}) b->release();
+    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -72,9 +71,17 @@ static WfFn wf16_pick(int G, int R) {
     return nullptr;
 }
 
+static WfFn wf16_pick_tb(int G, int R) {   // R % 4 == 0 shapes (wavefront16.hpp store groups)
+#define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<WF16_GLOBAL_TB, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
 static WfFn wf16_lookup(int algo, bool tb, int G, int R) {
     if (algo == WF_LOCAL) return wf16_pick<WF_LOCAL>(G, R);
-    if (algo == WF_GLOBAL) return tb ? wf16_pick<WF16_GLOBAL_TB>(G, R) : wf16_pick<WF_GLOBAL>(G, R);
+    if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return wf16_pick<WF_SEMI>(G, R);
 }
 
@@ -85,8 +92,10 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
 static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
     if (p.second_best || p.start_pos == 1) return false;
-    if (p.start_pos == 2 && (wf_algo != WF_GLOBAL || !getenv("GASALX_PACKED_TB")))   // packed traceback: WIP
-        return false;
+    if (p.start_pos == 2 && wf_algo != WF_GLOBAL) return false;   // packed traceback: GLOBAL only
+    // GLOBAL+TB reads the first pad query row, scored -K = -max(b, npen) there:
+    // exact for N-vs-base cells only if that equals the reference's -npen
+    if (p.start_pos == 2 && p.has_n_penalty && p.n_penalty < p.mismatch) return false;
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
     const int64_t a = p.match, b = p.mismatch, oe = (int64_t)p.gap_open + p.gap_extend, e = p.gap_extend;
@@ -160,7 +169,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             const uint32_t x8 = (wf_algo == WF_SEMI) ? t8 : q8, y8 = (wf_algo == WF_SEMI) ? q8 : t8;
             pl.G16 = 0;
             for (const Shape &sh : kShapes16)
-                if ((uint32_t)(sh.G * sh.R) >= x8) { pl.G16 = sh.G; pl.R16 = sh.R; break; }
+                if ((uint32_t)(sh.G * sh.R) >= x8 && !(pl.tb && sh.R % 4)) { pl.G16 = sh.G; pl.R16 = sh.R; break; }
             const uint32_t words = (y8 + 2 * pl.G16 + 4 + 3) & ~3u;   // odd-step tail + prefetch
             pl.lds16_stride = words * 8;                               // uint2 per position
             pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
@@ -245,8 +254,12 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         packed = 1;
     }
 
-    // traceback storage: one word per (8-column strip, padded query row)
-    const uint64_t tb_words = (uint64_t)pad8(shape.max_q) * (pad8(shape.max_t) / 8);
+    // traceback storage: one word per (8-column strip, padded query row); the
+    // packed GLOBAL+TB kernel's skewed uint16 layout needs (t8 + G + 2) / 4 words
+    // of 16 bits per row instead (wavefront16.hpp)
+    uint64_t tb_words = (uint64_t)pad8(shape.max_q) * (pad8(shape.max_t) / 8);
+    if (pl.packed16 && pl.tb)
+        tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pad8(shape.max_q) * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
     int32_t *qend = out.q_end, *tend = out.t_end;
     if (runs_tb) {
         HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
@@ -287,6 +300,10 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             const uint32_t grid16 = grid_for(n, ppb16);
             HIPCHK(ws.misc.reserve(grid16 + 64));
             P16.handled = ws.misc.as<uint8_t>();
+            if (pl.tb) {
+                HIPCHK(ws.aux.reserve((size_t)n * 4));
+                P16.tbfix = ws.aux.as<int32_t>();
+            }
             WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16);
             if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
             if (pl.lds16_bytes > 64 * 1024)
@@ -360,6 +377,19 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.cigar = out.cigar; T.n_ops = out.n_cigar_ops; T.n = n;
         T.a = p.match; T.b = p.mismatch; T.o = p.gap_open; T.e = p.gap_extend;
         T.is_local = p.algo == 3;
+        T.pk_flags = nullptr;
+        T.pk_ppb = 1; T.pk_R = 1; T.pk_rmagic = 0;
+        T.pk_fix = nullptr;
+        T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
+        T.qseq = qsrc; T.tseq = tsrc; T.toff = b.t_offsets; T.seq_packed = packed;
+        T.nval = p.n_code & 0xF; T.has_npen = p.has_n_penalty; T.npen = p.n_penalty;
+        if (pl.kind == PLAN_WAVEFRONT && pl.packed16) {
+            T.pk_flags = ws.misc.as<uint8_t>();
+            T.pk_ppb = kWavesPerBlock * (64 / pl.G16) * 2;
+            T.pk_R = pl.R16;
+            T.pk_rmagic = (uint32_t)((0x100000000ull + pl.R16 - 1) / pl.R16);
+            T.pk_fix = ws.aux.as<int32_t>();
+        }
         tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
         HIPCHK(hipGetLastError());
     }

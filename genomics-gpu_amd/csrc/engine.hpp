@@ -30,6 +30,7 @@ struct Workspace {
     DevBuf rows_h, rows_e, rev;     // generic kernels' row buffers
     DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
     DevBuf misc;                    // packed kernels: per-block "aligned here" flags
+    DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
     void release_all();
 };
 

@@ -417,7 +417,22 @@ struct TbArgs {
     uint32_t n;
     int32_t a, b, o, e;
     int32_t is_local;
+    // pairs aligned by the packed GLOBAL+TB kernel (wavefront16.hpp) use its
+    // skewed uint16 layout: flag per block of pk_ppb pairs, R rows per lane
+    const uint8_t *pk_flags;
+    uint32_t pk_ppb, pk_R, pk_rmagic;   // pk_rmagic = ceil(2^32 / pk_R)
+    const int32_t *pk_fix;              // H' at the start cell (row ql, column tl) when both are pads
+    int32_t sc_nn;                      // substitution score N vs N (GLOBAL rule)
+    // sequences (as the wavefront kernels read them) for the flags' s < 0 bit
+    const uint8_t *qseq, *tseq;
+    const uint32_t *toff;
+    int32_t seq_packed, nval, has_npen, npen;
 };
+
+__device__ __forceinline__ uint32_t tb_code(const uint8_t *seq, uint32_t off, uint32_t pos, int packed) {
+    if (!packed) return seq[off + pos] & 15u;
+    return (reinterpret_cast<const uint32_t *>(seq)[(off >> 3) + (pos >> 3)] >> (28 - ((pos & 7) << 2))) & 15u;
+}
 
 __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -429,6 +444,12 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int i, j, total = 0, curr = 0;
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
     else { i = (int)tl; j = (int)ql; }
+    const bool pk = A.pk_flags && A.pk_flags[tid / A.pk_ppb];
+    const uint16_t *tb16 = reinterpret_cast<const uint16_t *>(tb);
+    // packed kernel: the start cell (ql, tl), both pads, was scored with the pad
+    // row's -K instead of N==N.  Its E and F are exact, so with H' the value it
+    // did compute, the true cell takes the diagonal iff score + sc(N,N) >= H'.
+    bool fix_diag = pk && !A.is_local && (ql & 7) && (tl & 7) && A.score[tid] + A.sc_nn >= A.pk_fix[tid];
     uint8_t *out = A.cigar + A.qoff[tid];
     uint32_t prev = 0, opf = 0;
     int n_ops = 0, off = 0, count = 0, op_select = 3, op_shift = 0;
@@ -438,8 +459,24 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
         const int64_t strip = cell / (8 * (int64_t)q8);
         const int64_t rem = cell - strip * 8 * (int64_t)q8;
         uint32_t cell_op = 0;   // past the padded grid: 0
-        if (strip < (int64_t)tstrips)
-            cell_op = (tb[strip * q8 + (rem >> 3)] >> (28 - ((rem & 7) << 2))) & 15u;
+        if (strip < (int64_t)tstrips) {
+            if (pk) {
+                // wavefront16.hpp step_global_tb flags -> the reference's nibble
+                const uint32_t row = (uint32_t)(rem >> 3), col = (uint32_t)strip * 8 + (uint32_t)(rem & 7);
+                const uint32_t s = col + __umulhi(row, A.pk_rmagic);   // column + lane of the row
+                const uint32_t fl = (uint32_t)tb16[(uint64_t)(s >> 2) * q8 + row] >> (s & 3);
+                const uint32_t qc = tb_code(A.qseq, A.qoff[tid], row, A.seq_packed);
+                const uint32_t tc = tb_code(A.tseq, A.toff[tid], col, A.seq_packed);
+                int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
+                if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
+                const uint32_t u = fix_diag ? 0u : (fl & 1u);
+                fix_diag = false;
+                cell_op = (u ? ((fl & 16u) ? 2u : 3u) : (sc < 0 ? 1u : 0u)) | ((fl & 256u) ? 0u : 4u) |
+                          ((fl & 4096u) ? 0u : 8u);
+            } else {
+                cell_op = (tb[strip * q8 + (rem >> 3)] >> (28 - ((rem & 7) << 2))) & 15u;
+            }
+        }
         const uint32_t op = (cell_op >> op_shift) & (uint32_t)op_select;
         opf = (op == 0 || op_select == 3) ? op : (uint32_t)op_shift;
         op_select = (op == 0 || (op == 1 && op_select == 3)) ? 3 : 1;

@@ -46,6 +46,7 @@ struct WfArgs {
     uint8_t *handled;          // wavefront16: per block, 1 = aligned here, 0 = left to the int32 kernel
     const uint8_t *skip;       // int32 kernel: pairs whose packed block already aligned them
     uint32_t skip_ppb;         // pairs per packed block
+    int32_t *tbfix;            // wavefront16 GLOBAL+TB: H at the traceback start cell (ql, tl), see tb_kernel
 
 };
 

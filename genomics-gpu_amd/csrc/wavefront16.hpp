@@ -71,6 +71,12 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
+#ifndef GX_WF16_TB_WAVES
+#define GX_WF16_TB_WAVES 2   // GLOBAL + traceback kernel
+#endif
+#ifndef GX_WF16_TB_ROWSYNC
+#define GX_WF16_TB_ROWSYNC 0
+#endif
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
@@ -159,32 +165,30 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 }
 
 // ---------------------------------------------------------------------------
-// GLOBAL step with traceback nibbles (global.h:14-26): per cell
-//   low2 = (H == tmp) ? (s < 0) : ((H == F) ? 3 : 2);  bit2 = E extended;  bit3 = F extended
-// appended to dw (4 nibbles per 16-bit half; older ones fall off the top).
-// [x == 0] for x >= 0 is one saturating v_pk_sub_u16 (1 - x, clamped at 0).
+// GLOBAL step with traceback flags (global.h:14-26).  The
+// reference's nibble per cell is low2 = (H == tmp) ? (s < 0) : ((H == F) ? 3 : 2),
+// bit2 = E extended, bit3 = F extended; here each cell records four "differs"
+// flags and tb_kernel rebuilds the nibble (s < 0 it takes from the sequences):
+//   u = [H != tmp], w = [H != F], x = [E' != E - e], y = [F' != F - e].
+// A flag is bit 15 of (A + 0x7FFF) - B for A >= B (no carry/borrow crosses a
+// half); v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
+// v_and_or places them: step j of a 4-step window owns bits j (u), 4+j (w),
+// 8+j (x) and 12+j (y) of each 16-bit half of dw.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, __builtin_elementwise_sub_sat(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
-}
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-    return GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
-}
-__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {   // modular per half
-    return GX_AS(uint32_t, GX_AS(pk_u2, a) - GX_AS(pk_u2, b));
-}
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) { return (a & m) | b; }
 
 template <int R>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                                uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
                                                uint32_t &f_out, const uint32_t KK, const uint32_t OEK,
-                                               const uint32_t EXT, const uint32_t NN, const uint32_t ONE) {
-    const uint32_t TWO = ONE << 1;
-    uint32_t diag = diag_top, f = f_top;
+                                               const uint32_t EXT, const uint32_t NN, const int j) {
+    constexpr uint32_t C = 0x7FFF7FFFu;
+    const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
+    uint32_t diag = diag_top, f = f_top, tx = T.x, ty = T.y;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t v = __builtin_amdgcn_perm(ty, tx, xs[k]);
         const uint32_t t1 = pk_addnc(diag, v);
         const uint32_t tmp = pk_subnb(t1, KK);
         const uint32_t toe = pk_subnb(t1, OEK);
@@ -192,20 +196,19 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
         const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
         const uint32_t En = pk_max3(toe, em, NN);
         const uint32_t Fn = pk_max3(toe, fm, NN);
-        // direction nibble
-        const uint32_t z1 = pk_subsat_u16(ONE, pk_subnb(H, tmp));       // H came from the diagonal
-        const uint32_t z2 = pk_subsat_u16(ONE, pk_subnb(H, f));         // H == F
-        const uint32_t mx = pk_min_u16(pk_subsat_u16(KK, v), ONE);      // substitution score < 0
-        const uint32_t q = pk_addnc(z2, TWO);                            // 2 or 3
-        const uint32_t low = pk_mad_u16(z1, pk_sub16(mx, q), q);         // z1 ? mx : q
-        const uint32_t z4 = pk_subsat_u16(ONE, pk_subnb(En, em));       // E extended
-        const uint32_t z3 = pk_subsat_u16(ONE, pk_subnb(Fn, fm));       // F extended
-        const uint32_t nib = pk_mad_u16(z3, ONE << 3, pk_mad_u16(z4, ONE << 2, low));
-        dw[k] = pk_mad_u16(dw[k], ONE << 4, nib);
+        const uint32_t HC = H + C;
+        const uint32_t fu = HC - tmp, fw = HC - f, fx = (En + C) - em, fy = (Fn + C) - fm;
+        // bytes: [u, x] per half and [w, y] per half, 0x00 / 0xFF
+        const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
+        const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
+        dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
         Ek[k] = En;
         f = Fn;
         diag = Hin[k];
         Hout[k] = H;
+#if GX_WF16_TB_ROWSYNC
+        asm volatile("" : "+v"(f), "+v"(tx), "+v"(ty));   // schedule row by row (tuning variant)
+#endif
     }
     f_out = f;
 }
@@ -240,7 +243,7 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
 
 template <int ALGO_, int G, int R>
-__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
+__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
     constexpr int ALGO = GTB ? WF_GLOBAL : ALGO_;
@@ -289,6 +292,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
+            const uint32_t ylen = GTB ? __shfl(yl[h], ps * G) : 0u;
             uint32_t v = 0;
             const bool in = (int32_t)y0 >= 0 && y0 < yp;
             if (in) v = load4_codes(Y, yof, y0 >> 2, A.packed);
@@ -296,6 +300,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
             for (int j = 0; j < 4; ++j) {
                 const uint32_t l = in ? letter_of((v >> (8 * j)) & 15u, A.nval) : 6u;
                 other |= l == 5;
+                // traceback reads the first pad query row, scored here as -K: exact for
+                // pad x base columns, not for pad x real-N columns (N == N is a match)
+                if (GTB && !A.has_npen) other |= l == 4 && y0 + j < ylen;
+                if (GTB) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
                 tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
             }
         }
@@ -321,8 +329,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T
                     xs[k] = (xs[k] & ~(0xFFu << (16 * h))) | ((l + 4 * h) << (16 * h));
-                } else if (ALGO == WF_LOCAL) {
-                    other |= l != 4;                 // LOCAL pads must be N (scored -K here, dominated)
+                } else if (ALGO == WF_LOCAL || GTB) {
+                    other |= l != 4;                 // pads must be N (LOCAL: scored -K here, dominated)
                 }
             }
         }
@@ -403,21 +411,28 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
         const int32_t pb = P.base, go = A.o, ge = A.e;
         auto left = [=](int32_t r) -> uint32_t { return (uint32_t)(pb - (r <= 0 ? 0 : go + ge * r)) * 0x10001u; };
         uint32_t HA[R], HB[R], Ek[R];
-        uint32_t dw[GTB ? R : 1];                      // traceback nibbles: last 4 columns per half
+        uint32_t dw[GTB ? R : 1];                      // traceback nibbles: last 4 steps per half
 #pragma unroll
         for (int k = 0; k < R; ++k) { HA[k] = left((int32_t)(r0 + k)); HB[k] = HA[k]; Ek[k] = NN; }
 #pragma unroll
         for (int k = 0; k < (GTB ? R : 1); ++k) dw[k] = 0;
         uint32_t recvH = left((int32_t)r0 - 1), prevRecvH = recvH, recvF = NN, f = NN;
-        uint32_t kq_lane[2], kq[2];
-        int32_t score[2] = {0, 0};
+        uint32_t kq_lane[2], kq[2], kp_lane[2], kp[2];
+        bool fixable[2];
+        int32_t score[2] = {0, 0}, fixv[2] = {0, 0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             kq_lane[h] = (xl[h] - 1) / R;
             kq[h] = (xl[h] - 1) - kq_lane[h] * R;
+            // traceback starts at (row ql, column tl); when both are pad
+            // positions this kernel scores that cell -K instead of N==N, and records
+            // its H so tb_kernel can redo the cell's low two bits
+            fixable[h] = GTB && valid[h] && xl[h] < xpad[h] && yl[h] < ypad[h];
+            kp_lane[h] = xl[h] / R;
+            kp[h] = xl[h] - kp_lane[h] * R;
         }
         uint2 tnext = tcol[c + G];
-        auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+        auto half_step = [&](const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
             const uint2 T = tnext;
             tnext = tcol[cc + 1 + G];
             if (cc == -1) {
@@ -426,31 +441,18 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
 #pragma unroll
                 for (int k = 0; k < R; ++k) { Hout[k] = left(rr + k); Ek[k] = NN; }
                 f = NN;
+                if (GTB && j == 0) {
+#pragma unroll
+                    for (int k = 0; k < R; ++k) dw[k] = 0;   // the window's flags are OR-ed in
+                }
             } else {
                 const uint32_t dtop = (uint32_t)(pb - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
-                if constexpr (GTB) {
+                if constexpr (GTB)
                     step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, KK, OEK,
-                                      EXT, NN, A.one);
-                    if ((cc & 3) == 3 && cc >= 0) {
-                        // one word per (8-column strip, row), columns c..c+7 in nibbles 7..0 (global.h:170,262):
-                        // columns 0-3 of the strip are the word's high half, 4-7 its low half
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            if (valid[h] && (uint32_t)cc < ypad[h]) {
-                                uint16_t *dst = reinterpret_cast<uint16_t *>(
-                                                    A.tb + (uint64_t)pr[h] * A.tb_pair_words +
-                                                    (uint64_t)(cc >> 3) * xpad[h] + r0) +
-                                                ((cc & 4) ? 0 : 1);
-#pragma unroll
-                                for (int k = 0; k < R; ++k)
-                                    if (r0 + k < xpad[h]) dst[2 * k] = (uint16_t)(dw[k] >> (16 * h));
-                            }
-                        }
-                    }
-                } else {
+                                      EXT, NN, j);
+                else
                     step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KK, OEK, EXT,
                                    NN);
-                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
@@ -459,15 +461,55 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? 2 : GX_WF16_WAVES
                         for (int k = 0; k < R; ++k) v = (k == (int)kq[h]) ? Hout[k] : v;
                         score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb;
                     }
+                    if (fixable[h] && cc == (int32_t)yl[h] && lg == kp_lane[h]) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int k = 0; k < R; ++k) v = (k == (int)kp[h]) ? Hout[k] : v;
+                        fixv[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb;
+                    }
                 }
             }
             prevRecvH = recvH;
             recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
             recvF = (uint32_t)shr_lane((int32_t)f);
         };
-        for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-            half_step(c, HA, HB);
-            half_step(c + 1, HB, HA);
+        if constexpr (GTB) {
+            // Direction flags, skewed layout (read by tb_kernel): per pair, uint16
+            // [w][row] with w = (column + lane) / 4 holding the 4-step window's
+            // flags — every lane stores after the same steps, 4 rows per 8 bytes.
+            static_assert(R % 4 == 0, "GLOBAL+TB packed shapes need R % 4 == 0");
+            uint32_t W16[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
+            for (uint32_t s = 0; s < nsteps; s += 4, c += 4) {
+                half_step(c, 0, HA, HB);
+                half_step(c + 1, 1, HB, HA);
+                half_step(c + 2, 2, HA, HB);
+                half_step(c + 3, 3, HB, HA);
+                const uint32_t w = s >> 2;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (valid[h] && w < W16[h]) {
+                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                                        (uint64_t)w * xpad[h] + r0;
+                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+                        for (int k = 0; k < R; k += 4)
+                            if (r0 + k < xpad[h])
+                                *reinterpret_cast<uint2 *>(dst + k) =
+                                    make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
+                                               __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+                    }
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (fixable[h] && lg == kp_lane[h]) A.tbfix[pr[h]] = fixv[h];
+        } else {
+            for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
+                half_step(c, 0, HA, HB);
+                half_step(c + 1, 1, HB, HA);
+            }
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h)

@@ -216,7 +216,7 @@ def test_packed_input(engine):
 # ----------------------------------------------------- full-size configs ----
 def test_plan_is_wavefront_for_bench_configs():
     assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150).startswith("wavefront16_local")
-    assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300).startswith("wavefront_global_tb")
+    assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300).startswith("wavefront16_global_tb")
     assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL), 150, 182).startswith("wavefront16_semi")
     assert G.describe_plan(G.make_params(algo=G.GLOBAL), 300, 300).startswith("wavefront16_global")
 
