@@ -206,7 +206,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
 static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
 
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
-                 hipStream_t st, const BatchShape &shape) {
+                 hipStream_t st, const BatchShape &shape, uint64_t cigar_cap) {
     if (b.n_alns == 0 || b.q_bytes == 0 || b.t_bytes == 0) { set_error("empty batch"); return GASALX_EINVAL; }
     if ((b.q_bytes & 7) || (b.t_bytes & 7)) { set_error("batch bytes not a multiple of 8"); return GASALX_EINVAL; }
     if (!out.aln_score) { set_error("aln_score output required"); return GASALX_EINVAL; }
@@ -375,6 +375,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.score = out.aln_score; T.qend = qend; T.tend = tend;
         T.qstart = out.q_start; T.tstart = out.t_start;
         T.cigar = out.cigar; T.n_ops = out.n_cigar_ops; T.n = n;
+        T.cigar_cap = cigar_cap ? cigar_cap : b.q_bytes;
         T.a = p.match; T.b = p.mismatch; T.o = p.gap_open; T.e = p.gap_extend;
         T.is_local = p.algo == 3;
         T.pk_flags = nullptr;

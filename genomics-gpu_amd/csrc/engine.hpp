@@ -61,8 +61,9 @@ Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
 
 // Launch the full path for a device-resident batch on `stream`.
 // Returns GASALX_OK or an error code; sets the thread's last error message.
+// cigar_cap: bytes writable at out.cigar (0 = b.q_bytes)
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
-                 hipStream_t stream, const BatchShape &shape);
+                 hipStream_t stream, const BatchShape &shape, uint64_t cigar_cap = 0);
 
 int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipStream_t stream, uint32_t max_r,
                    uint32_t max_h);

@@ -413,6 +413,8 @@ struct TbArgs {
     const int32_t *score, *qend, *tend;
     int32_t *qstart, *tstart;
     uint8_t *cigar;
+    uint64_t cigar_cap;                 // writable bytes at cigar: a CIGAR longer than its slot
+                                        // runs into the next one, never past the buffer
     uint32_t *n_ops;
     uint32_t n;
     int32_t a, b, o, e;
@@ -429,9 +431,20 @@ struct TbArgs {
     int32_t seq_packed, nval, has_npen, npen;
 };
 
-__device__ __forceinline__ uint32_t tb_code(const uint8_t *seq, uint32_t off, uint32_t pos, int packed) {
-    if (!packed) return seq[off + pos] & 15u;
-    return (reinterpret_cast<const uint32_t *>(seq)[(off >> 3) + (pos >> 3)] >> (28 - ((pos & 7) << 2))) & 15u;
+// 8 codes of a sequence cached per thread (the walk moves one position at a time)
+__device__ __forceinline__ uint32_t tb_code(const uint8_t *seq, uint32_t off, uint32_t pos, int packed, uint2 &v,
+                                            int32_t &key) {
+    const int32_t k = (int32_t)(pos >> 3);
+    if (k != key) {
+        key = k;
+        v = packed ? make_uint2(reinterpret_cast<const uint32_t *>(seq)[(off >> 3) + (uint32_t)k], 0u)
+                   : *reinterpret_cast<const uint2 *>(seq + off + 8u * (uint32_t)k);
+    }
+    const uint32_t p = pos & 7u;
+    return packed ? (v.x >> (28 - 4 * p)) & 15u : ((p < 4 ? v.x : v.y) >> (8 * (p & 3u))) & 15u;
+}
+__device__ __forceinline__ uint32_t pick4(const uint4 &c, uint32_t k) {
+    return k == 0 ? c.x : k == 1 ? c.y : k == 2 ? c.z : c.w;
 }
 
 __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
@@ -451,22 +464,34 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     // did compute, the true cell takes the diagonal iff score + sc(N,N) >= H'.
     bool fix_diag = pk && !A.is_local && (ql & 7) && (tl & 7) && A.score[tid] + A.sc_nn >= A.pk_fix[tid];
     uint8_t *out = A.cigar + A.qoff[tid];
+    const uint64_t room = A.cigar_cap > A.qoff[tid] ? A.cigar_cap - A.qoff[tid] : 0;
+    auto put = [&](int at, uint32_t byte) { if ((uint64_t)at < room) out[at] = (uint8_t)byte; };
     uint32_t prev = 0, opf = 0;
     int n_ops = 0, off = 0, count = 0, op_select = 3, op_shift = 0;
+    // the walk reads one cell per step, mostly from consecutive rows: keep the
+    // 16-byte chunk it is in (4 rows of words / 8 rows of 16-bit flags) and the
+    // current 8 codes of each sequence, so most steps make no memory access
+    uint4 chunk = make_uint4(0u, 0u, 0u, 0u);
+    int64_t chunk_key = -1;
+    uint2 qv = make_uint2(0u, 0u), tv = make_uint2(0u, 0u);
+    int32_t qkey = -1, tkey = -1;
     while (i >= 0 && j >= 0) {
-        // get_tb.h:50-71: linear cell index over (strip, row, column)
-        const int64_t cell = ((int64_t)(i >> 3) * q8 << 3) + ((int64_t)j << 3) + (i & 7);
-        const int64_t strip = cell / (8 * (int64_t)q8);
-        const int64_t rem = cell - strip * 8 * (int64_t)q8;
+        // get_tb.h:50-71: linear cell index over (strip, row, column); a start
+        // one row past the padded query (j == q8) wraps to row 0 of the next strip
+        const bool wrap = j >= (int)q8;
+        const uint32_t strip = (uint32_t)(i >> 3) + (wrap ? 1u : 0u), row = wrap ? 0u : (uint32_t)j,
+                       c7 = (uint32_t)i & 7u;
         uint32_t cell_op = 0;   // past the padded grid: 0
-        if (strip < (int64_t)tstrips) {
+        if (strip < tstrips) {
             if (pk) {
                 // wavefront16.hpp step_global_tb flags -> the reference's nibble
-                const uint32_t row = (uint32_t)(rem >> 3), col = (uint32_t)strip * 8 + (uint32_t)(rem & 7);
+                const uint32_t col = strip * 8 + c7;
                 const uint32_t s = col + __umulhi(row, A.pk_rmagic);   // column + lane of the row
-                const uint32_t fl = (uint32_t)tb16[(uint64_t)(s >> 2) * q8 + row] >> (s & 3);
-                const uint32_t qc = tb_code(A.qseq, A.qoff[tid], row, A.seq_packed);
-                const uint32_t tc = tb_code(A.tseq, A.toff[tid], col, A.seq_packed);
+                const int64_t key = (int64_t)(s >> 2) * q8 + (row & ~7u);
+                if (key != chunk_key) { chunk = *reinterpret_cast<const uint4 *>(tb16 + key); chunk_key = key; }
+                const uint32_t fl = (pick4(chunk, (row & 7u) >> 1) >> (16 * (row & 1u) + (s & 3u))) & 0xFFFFu;
+                const uint32_t qc = tb_code(A.qseq, A.qoff[tid], row, A.seq_packed, qv, qkey);
+                const uint32_t tc = tb_code(A.tseq, A.toff[tid], col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
                 if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
                 const uint32_t u = fix_diag ? 0u : (fl & 1u);
@@ -474,7 +499,9 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 cell_op = (u ? ((fl & 16u) ? 2u : 3u) : (sc < 0 ? 1u : 0u)) | ((fl & 256u) ? 0u : 4u) |
                           ((fl & 4096u) ? 0u : 8u);
             } else {
-                cell_op = (tb[strip * q8 + (rem >> 3)] >> (28 - ((rem & 7) << 2))) & 15u;
+                const int64_t key = (int64_t)strip * q8 + (row & ~3u);
+                if (key != chunk_key) { chunk = *reinterpret_cast<const uint4 *>(tb + key); chunk_key = key; }
+                cell_op = (pick4(chunk, row & 3u) >> (28 - (c7 << 2))) & 15u;
             }
         }
         const uint32_t op = (cell_op >> op_shift) & (uint32_t)op_select;
@@ -484,7 +511,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
         if (count < 63 && opf == prev) {
             count++;
         } else {
-            if (count > 0) { out[off++] = (uint8_t)(prev | (uint32_t)(count << 2)); n_ops++; }
+            if (count > 0) { put(off++, prev | (uint32_t)(count << 2)); n_ops++; }
             count = 1;
         }
         if (A.is_local) {
@@ -496,11 +523,11 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
         i = (opf == 0 || opf == 1 || opf == 2) ? i - 1 : i;
         j = (opf == 0 || opf == 1 || opf == 3) ? j - 1 : j;
     }
-    out[off++] = (uint8_t)(prev | (uint32_t)(count << 2));
+    put(off++, prev | (uint32_t)(count << 2));
     n_ops++;
     if (!A.is_local) {
-        while (i >= 0) { const int rc = (i + 1) <= 63 ? (i + 1) : 63; out[off++] = (uint8_t)(2 | (rc << 2)); n_ops++; i -= 63; }
-        while (j >= 0) { const int rc = (j + 1) <= 63 ? (j + 1) : 63; out[off++] = (uint8_t)(3 | (rc << 2)); n_ops++; j -= 63; }
+        while (i >= 0) { const int rc = (i + 1) <= 63 ? (i + 1) : 63; put(off++, 2u | (uint32_t)(rc << 2)); n_ops++; i -= 63; }
+        while (j >= 0) { const int rc = (j + 1) <= 63 ? (j + 1) : 63; put(off++, 3u | (uint32_t)(rc << 2)); n_ops++; j -= 63; }
     } else {
         if (A.tstart) A.tstart[tid] = i;
         if (A.qstart) A.qstart[tid] = j;

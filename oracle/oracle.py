@@ -68,7 +68,10 @@ def align(batch, params: OrcParams, q_ops=None, t_ops=None, seed_scores=None, n_
     n = batch.n
     out = {k: np.full(n, SENTINEL, np.int32) for k in
            ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")}
-    cigar = np.zeros(batch.q_bytes, np.uint8)
+    # a CIGAR longer than its slot runs into the next; slack keeps the
+    # last pair's overrun inside the array
+    slack = int((np.asarray(batch.q_lens, np.int64) + np.asarray(batch.t_lens, np.int64)).max(initial=0)) + 64
+    cigar = np.zeros(batch.q_bytes + slack, np.uint8)
     n_ops = np.zeros(n, np.uint32)
     qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
     to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
@@ -85,7 +88,7 @@ def align(batch, params: OrcParams, q_ops=None, t_ops=None, seed_scores=None, n_
         _ptr(cigar), _ptr(n_ops), ctypes.c_int(n_threads))
     if rc != 0:
         raise ValueError(f"orc_aln_batch failed: {rc}")
-    out["cigar"] = cigar
+    out["cigar"] = cigar[:batch.q_bytes]
     out["n_ops"] = n_ops
     return out
 

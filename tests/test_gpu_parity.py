@@ -3,6 +3,8 @@ oracle on identical inputs.  Integer outputs must match bit-exactly; PairHMM
 within 1e-5 relative (BASELINE.json north_star)."""
 import os
 
+import zlib
+
 import numpy as np
 import pytest
 
@@ -229,7 +231,7 @@ def test_plan_is_wavefront_for_bench_configs():
 @pytest.mark.parametrize("alphabet", [b"ACGT", b"ACGTN", b"ACGTACGTACGTACGTN", b"ACGTRYacgt"])
 def test_packed_paths_with_declined_blocks(engine, algo, kw, alphabet):
     # blocks holding a code the packed kernel cannot score are re-aligned by the int32 kernel
-    rng = np.random.default_rng(hash((algo, alphabet)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(repr((algo, alphabet)).encode()) & 0xFFFF)
     qs, ts = helpers.random_pairs(rng, 1500, 1, 180, 1, 200, alphabet=alphabet)
     b = G.Batch.from_pairs(qs, ts)
     check(engine, b, algo=algo, **kw)
@@ -341,7 +343,7 @@ def test_pairhmm_random_long(engine):
 def test_packed_global_traceback(engine, scores, alphabet):
     # packed traceback words (and the int32 kernel's for declined blocks) feed the same get_tb walk
     a, bb, o, e = scores
-    rng = np.random.default_rng(hash((scores, alphabet)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(repr((scores, alphabet)).encode()) & 0xFFFF)
     qs, ts = helpers.random_pairs(rng, 700, 20, 310, 20, 310, alphabet=alphabet)
     kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB, match=a, mismatch=bb, gap_open=o, gap_extend=e)
     check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
