@@ -383,6 +383,16 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.pk_fix = nullptr;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
         T.qseq = qsrc; T.tseq = tsrc; T.toff = b.t_offsets; T.seq_packed = packed;
+        if (pl.kind == PLAN_WAVEFRONT && pl.packed16 && !pl.need_pack) {
+            // the walk writes CIGARs over the unpacked query batch when that is the
+            // cigar buffer (get_tb.h:94) but reads query codes: give it a copy
+            const uint8_t *c0 = out.cigar, *q0 = b.q_batch;
+            if (c0 < q0 + b.q_bytes && q0 < c0 + T.cigar_cap) {
+                HIPCHK(ws.packed_q.reserve(b.q_bytes));
+                HIPCHK(hipMemcpyAsync(ws.packed_q.p, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
+                T.qseq = ws.packed_q.as<uint8_t>();
+            }
+        }
         T.nval = p.n_code & 0xF; T.has_npen = p.has_n_penalty; T.npen = p.n_penalty;
         if (pl.kind == PLAN_WAVEFRONT && pl.packed16) {
             T.pk_flags = ws.misc.as<uint8_t>();
