@@ -97,6 +97,7 @@ def parse():
     ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: all-gather every rank's int32 scores (RCCL) inside each timed step")
     return ap.parse_args()
@@ -123,6 +124,32 @@ def cpu_baseline(batch, params_kw, budget_s):
     return {"value": round(cells / t_used / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
             "sample": f"first {done_pairs} pairs of the rank-0 batch ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
                       f"oracle/gasal_oracle.c OpenMP x{threads}"}
+
+
+def end_to_end(eng, kind, data, params, cells, reps=5):
+    """PCIe-inclusive rate through the host-buffer entry point (gasalx_align_host /
+    gasalx_pairhmm_host): host arrays in, H2D + kernels + D2H, results back in host
+    arrays.  Reported beside `value`, never as it."""
+    if kind == 5:
+        h = data
+        args = (h["reads"], h["read_offsets"], h["read_lens"], h["qm"], h["delta"], h["xiksi"], h["alpha"],
+                h["haps"], h["hap_offsets"], h["hap_lens"])
+        call = lambda: eng.pairhmm_host(*args)
+        path = "gasalx_pairhmm_host (pageable host arrays; H2D + kernel + D2H)"
+    else:
+        fields = ["score"] if params.algo == G.GLOBAL else ["score", "q_end", "t_end"]
+        call = lambda: eng.align_host(data, params, fields=fields)
+        path = ("gasalx_align_host (pageable host arrays; chunks of pairs on two streams, "
+                "H2D of chunk k+1 overlapping the kernels of chunk k)")
+    call()
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        call()
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    return {"value": round(cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_batch": round(dt * 1e3, 3),
+            "ms_all": [round(t * 1e3, 3) for t in times], "path": path}
 
 
 def main():
@@ -252,6 +279,9 @@ def main():
             "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
+        if world == 1 and not args.no_e2e:
+            out["end_to_end"] = end_to_end(eng, kind, h if kind == 5 else batch, None if kind == 5 else params,
+                                           cells_per_step)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = (cpu_baseline_pairhmm(h, args.cpu_seconds) if kind == 5
                                    else cpu_baseline(batch, pkw, args.cpu_seconds))

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -11,16 +12,32 @@
 #include "engine.hpp"
 #include "gasalx.h"
 
+// One stage of the host-staged pipeline (gasalx_align_host on large batches):
+// its own stream, workspace and device copies of one chunk of pairs.
+struct HostSlot {
+    hipStream_t st = nullptr;
+    gx::Workspace ws;
+    gx::DevBuf q, t, meta, cig;
+    std::vector<uint8_t> hmeta;   // host image of the chunk's per-pair region (meta)
+    void release() {
+        ws.release_all();
+        for (gx::DevBuf *b : {&q, &t, &meta, &cig}) b->release();
+        if (st) { (void)hipStreamSynchronize(st); (void)hipStreamDestroy(st); st = nullptr; }
+    }
+};
+
 struct gasalx_engine {
     int device = 0;
     hipStream_t stream = nullptr;
     gx::Workspace ws;
+    HostSlot slot[2];
     // staging for the host-to-host entry points
     gx::DevBuf q, t, qo, to, ql, tl, qop, top, seed;
     gx::DevBuf o_score, o_qe, o_te, o_qs, o_ts, o_s2, o_qe2, o_te2, o_cig, o_nops, lens_max;
     gx::DevBuf h_reads, h_ro, h_rl, h_qm, h_de, h_xi, h_al, h_haps, h_ho, h_hl, h_res;
     void release() {
         ws.release_all();
+        for (HostSlot &s : slot) s.release();
         for (gx::DevBuf *b : {&q, &t, &qo, &to, &ql, &tl, &qop, &top, &seed, &o_score, &o_qe, &o_te, &o_qs, &o_ts,
                               &o_s2, &o_qe2, &o_te2, &o_cig, &o_nops, &lens_max, &h_reads, &h_ro, &h_rl, &h_qm,
                               &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res})
@@ -140,6 +157,147 @@ int gasalx_align_device(gasalx_engine *eng, const gasalx_params *params, const g
     return gx::align_device(eng->ws, *params, *b, *out, st, shape);
 }
 
+namespace {
+
+uint32_t pad8u(uint32_t x) { return (x + 7u) & ~7u; }
+
+// Sequences laid out back to back from offset 0 (what gasal_host_batch_fill
+// produces): chunks of pairs then own contiguous byte ranges.
+bool contiguous(const uint32_t *off, const uint32_t *len, uint32_t n, uint32_t bytes) {
+    uint64_t at = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (off[i] != at) return false;
+        at += pad8u(len[i]);
+    }
+    return at == bytes;
+}
+
+// Large host batches: chunks of pairs alternate between two streams, so the
+// H2D copy of chunk k+1 overlaps the kernels of chunk k (the copies run at
+// PCIe speed from pageable memory on this platform, tools/h2d_probe.cpp).
+// Per chunk: two sequence copies plus ONE copy of everything per-pair
+// (rebased offsets, lengths, ops, seeds, the caller's output contents) and
+// ONE copy back of the per-pair outputs.
+int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *hb,
+                         const gasalx_results *ho, uint32_t chunk) {
+    const uint32_t n = hb->n_alns;
+    const bool tb = params->start_pos == 2;
+    const uint32_t mq = hb->max_q_len ? hb->max_q_len : host_max(hb->q_lens, n);
+    const uint32_t mt = hb->max_t_len ? hb->max_t_len : host_max(hb->t_lens, n);
+    int32_t *const hout[8] = {ho->aln_score, ho->q_end, ho->t_end, ho->q_start,
+                              ho->t_start, ho->aln_score2, ho->q_end2, ho->t_end2};
+    uint32_t *const hnops = tb ? ho->n_cigar_ops : nullptr;
+    for (HostSlot &s : eng->slot) {
+        if (!s.st) CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+        s.ws.device = eng->device;
+    }
+    // per-pair region of a chunk of m pairs: 4-byte columns, 16-byte aligned
+    auto col = [](uint32_t m) { return ((size_t)m * 4 + 15) & ~(size_t)15; };
+    auto bcol = [](uint32_t m) { return ((size_t)m + 15) & ~(size_t)15; };
+    struct Pending { uint32_t i0, i1; uint64_t qlo, qhi; size_t out_at, out_len; bool live; } pend[2] = {};
+    auto drain = [&](int k) -> int {   // the slot's previous chunk: results back to the caller
+        Pending &pp = pend[k];
+        if (!pp.live) return GASALX_OK;
+        HostSlot &s = eng->slot[k];
+        const uint32_t m = pp.i1 - pp.i0;
+        if (pp.out_len)
+            CK(hipMemcpyAsync(s.hmeta.data() + pp.out_at, s.meta.as<uint8_t>() + pp.out_at, pp.out_len,
+                              hipMemcpyDeviceToHost, s.st));
+        if (tb && ho->cigar)
+            CK(hipMemcpyAsync(ho->cigar + pp.qlo, s.cig.p, pp.qhi - pp.qlo, hipMemcpyDeviceToHost, s.st));
+        CK(hipStreamSynchronize(s.st));
+        size_t at = pp.out_at;
+        for (int f = 0; f < 8; f++)
+            if (hout[f]) { std::memcpy(hout[f] + pp.i0, s.hmeta.data() + at, m * 4ull); at += col(m); }
+        if (hnops) std::memcpy(hnops + pp.i0, s.hmeta.data() + at, m * 4ull);
+        pp.live = false;
+        return GASALX_OK;
+    };
+    int rc = GASALX_OK, k = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += chunk, k ^= 1) {
+        const uint32_t i1 = std::min(n, i0 + chunk), m = i1 - i0;
+        HostSlot &s = eng->slot[k];
+        if ((rc = drain(k))) return rc;
+        const uint64_t qlo = hb->q_offsets[i0], qhi = (uint64_t)hb->q_offsets[i1 - 1] + pad8u(hb->q_lens[i1 - 1]);
+        const uint64_t tlo = hb->t_offsets[i0], thi = (uint64_t)hb->t_offsets[i1 - 1] + pad8u(hb->t_lens[i1 - 1]);
+        // host image of the per-pair region
+        size_t at = 0;
+        const size_t a_qo = at; at += col(m);
+        const size_t a_to = at; at += col(m);
+        const size_t a_ql = at; at += col(m);
+        const size_t a_tl = at; at += col(m);
+        const size_t a_qop = at; if (hb->q_ops) at += bcol(m);
+        const size_t a_top = at; if (hb->t_ops) at += bcol(m);
+        const size_t a_seed = at; if (hb->seed_scores) at += col(m);
+        const size_t out_at = at;
+        size_t a_out[8];
+        for (int f = 0; f < 8; f++) { a_out[f] = at; if (hout[f]) at += col(m); }
+        const size_t a_nops = at; if (hnops) at += col(m);
+        const size_t total = at;
+        s.hmeta.resize(total);
+        uint8_t *h = s.hmeta.data();
+        uint32_t *qo = reinterpret_cast<uint32_t *>(h + a_qo), *to = reinterpret_cast<uint32_t *>(h + a_to);
+        for (uint32_t i = 0; i < m; i++) {
+            qo[i] = hb->q_offsets[i0 + i] - (uint32_t)qlo;
+            to[i] = hb->t_offsets[i0 + i] - (uint32_t)tlo;
+        }
+        std::memcpy(h + a_ql, hb->q_lens + i0, m * 4ull);
+        std::memcpy(h + a_tl, hb->t_lens + i0, m * 4ull);
+        if (hb->q_ops) std::memcpy(h + a_qop, hb->q_ops + i0, m);
+        if (hb->t_ops) std::memcpy(h + a_top, hb->t_ops + i0, m);
+        if (hb->seed_scores) std::memcpy(h + a_seed, hb->seed_scores + i0, m * 4ull);
+        for (int f = 0; f < 8; f++)   // the caller's contents: fields the reference does not write come back unchanged
+            if (hout[f]) std::memcpy(h + a_out[f], hout[f] + i0, m * 4ull);
+        if (hnops) std::memcpy(h + a_nops, hnops + i0, m * 4ull);
+        CK(s.meta.reserve(total + 16));
+        uint8_t *dm = s.meta.as<uint8_t>();
+        uint8_t *p8;
+        if ((rc = stage_in(s.q, hb->q_batch + qlo, qhi - qlo, s.st, &p8))) return rc;
+        gasalx_batch db = *hb;
+        db.q_batch = p8;
+        if ((rc = stage_in(s.t, hb->t_batch + tlo, thi - tlo, s.st, &p8))) return rc;
+        db.t_batch = p8;
+        CK(hipMemcpyAsync(dm, h, total, hipMemcpyHostToDevice, s.st));
+        db.q_offsets = reinterpret_cast<uint32_t *>(dm + a_qo);
+        db.t_offsets = reinterpret_cast<uint32_t *>(dm + a_to);
+        db.q_lens = reinterpret_cast<uint32_t *>(dm + a_ql);
+        db.t_lens = reinterpret_cast<uint32_t *>(dm + a_tl);
+        db.q_ops = hb->q_ops ? dm + a_qop : nullptr;
+        db.t_ops = hb->t_ops ? dm + a_top : nullptr;
+        db.seed_scores = hb->seed_scores ? reinterpret_cast<uint32_t *>(dm + a_seed) : nullptr;
+        db.q_bytes = (uint32_t)(qhi - qlo);
+        db.t_bytes = (uint32_t)(thi - tlo);
+        db.n_alns = m;
+        db.max_q_len = mq;
+        db.max_t_len = mt;
+        gasalx_results dout;
+        std::memset(&dout, 0, sizeof(dout));
+        int32_t **dfield[8] = {&dout.aln_score, &dout.q_end, &dout.t_end, &dout.q_start,
+                               &dout.t_start, &dout.aln_score2, &dout.q_end2, &dout.t_end2};
+        for (int f = 0; f < 8; f++) *dfield[f] = hout[f] ? reinterpret_cast<int32_t *>(dm + a_out[f]) : nullptr;
+        if (hnops) dout.n_cigar_ops = reinterpret_cast<uint32_t *>(dm + a_nops);
+        if (tb && ho->cigar) {
+            CK(s.cig.reserve(qhi - qlo + 16));
+            dout.cigar = s.cig.as<uint8_t>();
+        }
+        gx::BatchShape shape;
+        shape.max_q = mq;
+        shape.max_t = mt;
+        if ((rc = gx::align_device(s.ws, *params, db, dout, s.st, shape))) {
+            for (HostSlot &x : eng->slot) (void)hipStreamSynchronize(x.st);
+            return rc;
+        }
+        pend[k] = {i0, i1, qlo, qhi, out_at, total - out_at, true};
+    }
+    for (int j = 0; j < 2; j++) {
+        k ^= 1;
+        if ((rc = drain(k))) return rc;
+    }
+    return GASALX_OK;
+}
+
+}  // namespace
+
 int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *hb,
                       const gasalx_results *ho) {
     if (!eng || !valid_params(params) || !hb || !ho) { gx::set_error("null argument"); return GASALX_EINVAL; }
@@ -150,6 +308,13 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     CK(hipSetDevice(eng->device));
     hipStream_t st = eng->stream;
     const uint32_t n = hb->n_alns;
+    // large batches in the standard layout go through the two-stream pipeline
+    // the traceback walk is latency-bound per chunk whatever its size: two chunks for TB
+    const uint32_t chunk = std::max<uint32_t>(16384, params->start_pos == 2 ? (n + 1) / 2 : (n + 7) / 8);
+    static const bool single = std::getenv("GASALX_HOST_SINGLE") != nullptr;   // A/B knob
+    if (!single && n >= 2 * chunk && !params->is_packed && contiguous(hb->q_offsets, hb->q_lens, n, hb->q_bytes) &&
+        contiguous(hb->t_offsets, hb->t_lens, n, hb->t_bytes))
+        return align_host_pipelined(eng, params, hb, ho, chunk);
     gasalx_batch db = *hb;
     int rc = 0;
     uint8_t *p8; uint32_t *p32;

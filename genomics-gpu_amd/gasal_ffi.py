@@ -181,17 +181,20 @@ class Engine:
         except Exception:
             pass
 
-    def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None):
+    def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None, fields=None):
+        """fields: the result arrays to request (default all; the rest are passed as NULL)."""
         n = batch.n
-        out = {k: np.full(n, SENTINEL, np.int32) for k in OUT_FIELDS}
-        cigar = np.zeros(batch.q_bytes, np.uint8)
-        n_ops = np.zeros(n, np.uint32)
+        out = {k: np.full(n, SENTINEL, np.int32) for k in (OUT_FIELDS if fields is None else fields)}
+        tb = params.start_pos == WITH_TB          # CIGAR buffers only when the reference fills them
+        cigar = np.zeros(batch.q_bytes if tb else 0, np.uint8)
+        n_ops = np.zeros(n if tb else 0, np.uint32)
         qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
         to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
         sd = None if seed_scores is None else np.ascontiguousarray(seed_scores, np.uint32)
         cb = CBatch(_p(batch.q_data), _p(batch.q_offsets), _p(batch.q_lens), _p(batch.t_data), _p(batch.t_offsets),
                     _p(batch.t_lens), batch.q_bytes, batch.t_bytes, n, _p(qo), _p(to), _p(sd), 0, 0)
-        cr = CResults(*(_p(out[k]) for k in OUT_FIELDS), _p(cigar), _p(n_ops))
+        cr = CResults(*(_p(out[k]) if k in out else None for k in OUT_FIELDS), _p(cigar) if tb else None,
+                      _p(n_ops) if tb else None)
         _check(lib().gasalx_align_host(self._h, ctypes.byref(params), ctypes.byref(cb), ctypes.byref(cr)),
                "align_host")
         out["cigar"] = cigar

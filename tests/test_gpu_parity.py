@@ -347,3 +347,22 @@ def test_packed_global_traceback(engine, scores, alphabet):
     qs, ts = helpers.random_pairs(rng, 700, 20, 310, 20, 310, alphabet=alphabet)
     kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB, match=a, mismatch=bb, gap_open=o, gap_extend=e)
     check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
+
+
+@pytest.mark.parametrize("kw", [dict(algo=G.LOCAL), dict(algo=G.GLOBAL, start_pos=G.WITH_TB),
+                                dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET),
+                                dict(algo=G.LOCAL, start_pos=G.WITH_TB)])
+def test_host_pipeline_chunks(engine, kw):
+    # >= 2 x 16384 pairs in the back-to-back layout: gasalx_align_host splits the batch
+    # into chunks on two streams (capi.cpp align_host_pipelined); results and CIGARs
+    # must land exactly where the single-shot path puts them
+    rng = np.random.default_rng(0x919E)
+    qs, ts = helpers.random_pairs(rng, 40000, 8, 72, 8, 80, alphabet=b"ACGTACGTACGTN")
+    batch = G.Batch.from_pairs(qs, ts)
+    tb = kw.get("start_pos") == G.WITH_TB
+    if tb:
+        batch = no_cigar_overflow(batch, **kw)
+    q_ops = rng.integers(0, 4, batch.n).astype(np.uint8) if kw["algo"] == G.LOCAL and not tb else None
+    t_ops = rng.integers(0, 4, batch.n).astype(np.uint8) if q_ops is not None else None
+    assert batch.n >= 2 * 16384
+    check(engine, batch, q_ops=q_ops, t_ops=t_ops, cigar=tb, **kw)
