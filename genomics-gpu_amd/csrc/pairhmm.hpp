@@ -59,33 +59,39 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     __syncthreads();
     const uint8_t *hap = wl + slot * stride;
 
-    // the lane's read rows and their parameters (tile_1.cu:89-118)
-    const uint32_t r0 = lg * RR;
+    // the lane's read rows and their parameters (tile_1.cu:89-118).  Rows are
+    // bottom-aligned: the group covers rows [R - G*RR, R), so the read's last row
+    // is always the bottom row of lane G-1 and the result sum needs no per-row
+    // select.  The rows above row 0 are "virtual": prior 0, delta 0, xi 0 and D
+    // decay 1.0, so from the boundary (M, I, D) = (0, 0, D0) they pass exactly
+    // (0, 0, D0) down at every column.
+    const int32_t r0 = (int32_t)(lg * RR) - (int32_t)(G * RR) + (int32_t)R;
     uint32_t rb[RR];
-    float qm1[RR], qm3[RR], de[RR], xi[RR], al[RR];
+    float qm1[RR], qm3[RR], de[RR], xi[RR], al[RR], dk[RR];
     float Mk[RR], Dk[RR], MM[RR];
+    const float D0 = valid && H ? __fdiv_rn(c0, (float)H) : 0.f;      // constant[0]/(float)H
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
-        const uint32_t i = r0 + k;
-        const bool in = valid && i < R;
+        const int32_t i = r0 + k;
+        const bool in = valid && i >= 0;
         const float q = in ? A.qm[ro + i] : 0.f;
         rb[k] = in ? A.reads[ro + i] : 0x100u;
-        qm1[k] = __fsub_rn(1.0f, q);                 // Qm_1 = constant[1] - Qm
-        qm3[k] = __fdiv_rn(q, 3.0f);                 // fdividef(Qm, 3) (<= 2 ulp in the reference)
+        qm1[k] = in ? __fsub_rn(1.0f, q) : 0.f;     // Qm_1 = constant[1] - Qm
+        qm3[k] = in ? __fdiv_rn(q, 3.0f) : 0.f;     // fdividef(Qm, 3) (<= 2 ulp in the reference)
         de[k] = in ? A.delta[ro + i] : 0.f;
         xi[k] = in ? A.xiksi[ro + i] : 0.f;
         al[k] = in ? A.alpha[ro + i] : 0.f;
-        Mk[k] = 0.f; Dk[k] = 0.f; MM[k] = 0.f;
+        dk[k] = in ? c01 : 1.0f;
+        Mk[k] = 0.f;
+        Dk[k] = in ? 0.f : D0;
+        MM[k] = i == 0 ? __fmul_rn(c09, D0) : 0.f;                     // first row's MMID (:117)
     }
-    const float D0 = valid && H ? __fdiv_rn(c0, (float)H) : 0.f;      // constant[0]/(float)H
-    if (lg == 0) MM[0] = __fmul_rn(c09, D0);                           // first row's MMID (:117)
 
     uint32_t hmax = H;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, m));
     const uint32_t nsteps = hmax + G - 1;
-    const uint32_t last_lane = R ? (R - 1) / RR : 0;
-    const uint32_t klast = R ? (R - 1) - last_lane * RR : 0;
+    const bool bottom = lg == G - 1;
     float acc = 0.f;
     float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
 
@@ -106,16 +112,16 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
                 const float MIIDD = __fmul_rn(c09, MID);
                 const float Mn = __fmul_rn(aa, MM[k]);
                 const float In = __fmaf_rn(MU, de[k], IIMI);
-                const float Dn = __fmaf_rn(Dk[k], c01, DDM);
+                const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
                 MM[k] = __fmaf_rn(al[k], MU, MIIDD);
                 Mk[k] = Mn; Dk[k] = Dn;
-                if (lg == last_lane && k == (int)klast) acc = __fadd_rn(acc, __fadd_rn(Mn, In));
                 MU = Mn; IU = In; DU = Dn;
             }
+            if (bottom) acc = __fadd_rn(acc, __fadd_rn(MU, IU));       // row R-1, column j (:166-167)
         }
         rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
     }
-    if (valid && lg == last_lane) A.result[pair] = acc;
+    if (valid && bottom) A.result[pair] = acc;
 }
 
 }  // namespace gx

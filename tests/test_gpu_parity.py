@@ -366,3 +366,18 @@ def test_host_pipeline_chunks(engine, kw):
     t_ops = rng.integers(0, 4, batch.n).astype(np.uint8) if q_ops is not None else None
     assert batch.n >= 2 * 16384
     check(engine, batch, q_ops=q_ops, t_ops=t_ops, cigar=tb, **kw)
+
+
+def test_pairhmm_edge_lengths(engine):
+    # bottom-aligned read rows (pairhmm.hpp): reads of 1 row, exact multiples of the
+    # lane rows, one more / one less, haplotypes shorter than the read, varied quals
+    rng = np.random.default_rng(0xE1)
+    pairs = []
+    for R in (1, 2, 7, 8, 9, 31, 32, 33, 64, 65, 127, 128, 129, 255, 256):
+        for H in (1, 2, max(1, R - 1), R, R + 1, 500):
+            hap = helpers.random_seq(rng, H).decode()
+            read = helpers.random_seq(rng, R).decode() if rng.random() < 0.5 else (hap * (R // H + 1))[:R]
+            pairs.append(dict(read=read, hap=hap, bq=rng.integers(0, 60, R), iq=rng.integers(10, 60, R),
+                              dq=rng.integers(10, 60, R)))
+    args = _hmm_batch(pairs)
+    np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
