@@ -161,10 +161,6 @@ namespace {
 
 uint32_t pad8u(uint32_t x) { return (x + 7u) & ~7u; }
 
-// fn(a, b) over [0, m).  (Splitting the host image across threads measured
-// slower: the copy engine, not this loop, bounds the pipeline.)
-extern "C++" template <class F>
-void par_ranges(uint32_t m, F &&fn) { fn(0u, m); }
 
 // Sequences laid out back to back from offset 0 (what gasal_host_batch_fill
 // produces): chunks of pairs then own contiguous byte ranges.
@@ -216,12 +212,10 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         if (tb && ho->cigar)
             CK(hipMemcpyAsync(ho->cigar + pp.qlo, s.cig.p, pp.qhi - pp.qlo, hipMemcpyDeviceToHost, s.st));
         CK(hipStreamSynchronize(s.st));
-        par_ranges(m, [&](uint32_t a, uint32_t b) {
-            size_t at = pp.out_at;
-            for (int f = 0; f < 8; f++)
-                if (hout[f]) { std::memcpy(hout[f] + pp.i0 + a, s.hmeta.data() + at + 4 * a, (b - a) * 4ull); at += col(m); }
-            if (hnops) std::memcpy(hnops + pp.i0 + a, s.hmeta.data() + at + 4 * a, (b - a) * 4ull);
-        });
+        size_t at = pp.out_at;
+        for (int f = 0; f < 8; f++)
+            if (hout[f]) { std::memcpy(hout[f] + pp.i0, s.hmeta.data() + at, m * 4ull); at += col(m); }
+        if (hnops) std::memcpy(hnops + pp.i0, s.hmeta.data() + at, m * 4ull);
         pp.live = false;
         return GASALX_OK;
     };
@@ -249,23 +243,20 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         s.hmeta.resize(total);
         uint8_t *h = s.hmeta.data();
         uint32_t *qo = reinterpret_cast<uint32_t *>(h + a_qo), *to = reinterpret_cast<uint32_t *>(h + a_to);
-        par_ranges(m, [&](uint32_t a, uint32_t b) {
-            for (uint32_t i = a; i < b; i++) {
-                qo[i] = hb->q_offsets[i0 + i] - (uint32_t)qlo;
-                to[i] = hb->t_offsets[i0 + i] - (uint32_t)tlo;
-            }
-            const size_t c = b - a;
-            std::memcpy(h + a_ql + 4 * a, hb->q_lens + i0 + a, c * 4);
-            std::memcpy(h + a_tl + 4 * a, hb->t_lens + i0 + a, c * 4);
-            if (hb->q_ops) std::memcpy(h + a_qop + a, hb->q_ops + i0 + a, c);
-            if (hb->t_ops) std::memcpy(h + a_top + a, hb->t_ops + i0 + a, c);
-            if (hb->seed_scores) std::memcpy(h + a_seed + 4 * a, hb->seed_scores + i0 + a, c * 4);
-            // the caller's contents, so fields the reference does not write come back
-            // unchanged; fields every kernel of this algo writes need no copy in
-            for (int f = 0; f < 8; f++)
-                if (hout[f] && !written[f]) std::memcpy(h + a_out[f] + 4 * a, hout[f] + i0 + a, c * 4);
-            if (hnops) std::memcpy(h + a_nops + 4 * a, hnops + i0 + a, c * 4);
-        });
+        for (uint32_t i = 0; i < m; i++) {
+            qo[i] = hb->q_offsets[i0 + i] - (uint32_t)qlo;
+            to[i] = hb->t_offsets[i0 + i] - (uint32_t)tlo;
+        }
+        std::memcpy(h + a_ql, hb->q_lens + i0, m * 4ull);
+        std::memcpy(h + a_tl, hb->t_lens + i0, m * 4ull);
+        if (hb->q_ops) std::memcpy(h + a_qop, hb->q_ops + i0, m);
+        if (hb->t_ops) std::memcpy(h + a_top, hb->t_ops + i0, m);
+        if (hb->seed_scores) std::memcpy(h + a_seed, hb->seed_scores + i0, m * 4ull);
+        // the caller's contents, so fields the reference does not write come back
+        // unchanged; fields every kernel of this algo writes need no copy in
+        for (int f = 0; f < 8; f++)
+            if (hout[f] && !written[f]) std::memcpy(h + a_out[f], hout[f] + i0, m * 4ull);
+        if (hnops) std::memcpy(h + a_nops, hnops + i0, m * 4ull);
         CK(s.meta.reserve(total + 16));
         uint8_t *dm = s.meta.as<uint8_t>();
         uint8_t *p8;
