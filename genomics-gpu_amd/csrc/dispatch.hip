@@ -108,18 +108,21 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
         *vmin = 0;
         return base + 255 + a + k + 64 <= 0x7BFF;
     }
-    int64_t k, top;
+    int64_t k, top, drift = 0;
     if (wf_algo == WF_SEMI) {
         if (p.tail != 2) return false;                         // TAIL=TARGET only (last query row)
         if (oe < b || oe < npen) return false;                 // table offset K = OE
         k = oe;
     } else {
-        k = std::max(b, npen);
+        drift = (std::max(b, npen) + 1) / 2;                   // GLOBAL: values drift by D per anti-diagonal,
+        k = 2 * drift;                                         // table offset K = 2D (pk16_params)
     }
     if (a + k > 255) return false;
-    const int64_t v = 4 * oe + k + e * (q8 + t8) + 64;         // below every reachable value
+    const int64_t v = 4 * oe + k + e * (q8 + t8) + 2 * drift + 64;   // below every reachable value
     const int64_t neg = 0x400 + 2 * e + 16;
-    top = neg + v + a * std::min(q8, t8) + a + k + oe + 64;
+    // + the drift over the anti-diagonals a lane sweeps (incl. up to 64+4 steps of
+    //   garbage before the reset / after the last column)
+    top = neg + v + a * std::min(q8, t8) + a + k + oe + 64 + drift * (q8 + t8 + 2 * 64 + 8);
     if (top > 0x7BFF) return false;
     *vmin = (int32_t)v;
     return true;

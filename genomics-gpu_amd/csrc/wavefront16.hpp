@@ -95,6 +95,7 @@ struct Pk16 {
     int32_t k;      // table offset
     int32_t base;   // stored value of 0
     int32_t neg;    // stored "minus infinity" (below every reachable value)
+    int32_t drift;  // GLOBAL: a value of cell (r, c) is stored + drift*(r + c)
 };
 template <int ALGO>
 __device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
@@ -104,8 +105,14 @@ __device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
         P.k = max(A.b, A.has_npen ? A.npen : 0);
         P.base = 0x0400 + OE + P.k + 16;
         P.neg = P.base;
+        P.drift = 0;
     } else {
         P.k = (ALGO == WF_SEMI) ? OE : max(A.b, A.has_npen ? A.npen : 0);
+        P.drift = 0;
+        if (ALGO == WF_GLOBAL) {       // table offset 2*drift: diag + byte is tmp itself
+            P.drift = (P.k + 1) >> 1;
+            P.k = 2 * P.drift;
+        }
         P.neg = 0x0400 + 2 * A.e + 16;
         P.base = P.neg + A.vmin;
     }
@@ -143,18 +150,21 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
 // ---------------------------------------------------------------------------
 // GLOBAL step: as LOCAL without the floor at 0 and without keys.
 // ---------------------------------------------------------------------------
+// Values drift: cell (r, c) is stored as value + B + D*(r+c) with table offset
+// K = 2D, so diag + byte is tmp itself (no subtraction), and E and F, which move
+// one anti-diagonal, take toe = tmp - (OE - D) and an extend of e - D (32-bit
+// adds/subtracts of a signed per-half constant, exact either way round).
 template <int R>
 __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                             const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
-                                            uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t KK,
-                                            const uint32_t OEK, const uint32_t EXT, const uint32_t NN) {
+                                            uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t OED,
+                                            const uint32_t EXT, const uint32_t NN) {
     uint32_t diag = diag_top, f = f_top;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
-        const uint32_t t1 = pk_addnc(diag, v);
-        const uint32_t tmp = pk_subnb(t1, KK);
-        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t tmp = pk_addnc(diag, v);
+        const uint32_t toe = pk_subnb(tmp, OED);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
         Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), NN);
         f = pk_max3(toe, pk_subnb(f, EXT), NN);
@@ -181,17 +191,16 @@ template <int R>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                                uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
-                                               uint32_t &f_out, const uint32_t KK, const uint32_t OEK,
-                                               const uint32_t EXT, const uint32_t NN, const int j) {
+                                               uint32_t &f_out, const uint32_t OED, const uint32_t EXT,
+                                               const uint32_t NN, const int j) {
     constexpr uint32_t C = 0x7FFF7FFFu;
     const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
     uint32_t diag = diag_top, f = f_top, tx = T.x, ty = T.y;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(ty, tx, xs[k]);
-        const uint32_t t1 = pk_addnc(diag, v);
-        const uint32_t tmp = pk_subnb(t1, KK);
-        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t tmp = pk_addnc(diag, v);          // drift: see step_global
+        const uint32_t toe = pk_subnb(tmp, OED);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
         const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
         const uint32_t En = pk_max3(toe, em, NN);
@@ -407,9 +416,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
         // boundaries (global.h:57-71, Q2): H(r,-1) = -(o+e*r) (0 for r = 0), E = -inf;
         // top: H(-1,c-1) = -(o+e*c) (0 for c = 0), F = -inf.  Lanes sweep garbage
         // columns c < -1 first and reset to the left boundary at c = -1.
-        const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
-        const int32_t pb = P.base, go = A.o, ge = A.e;
-        auto left = [=](int32_t r) -> uint32_t { return (uint32_t)(pb - (r <= 0 ? 0 : go + ge * r)) * 0x10001u; };
+        const int32_t pb = P.base, go = A.o, ge = A.e, D = P.drift;
+        // signed per-half constants: a 32-bit subtract of c*0x10001 is exact per half for either sign
+        const uint32_t OED = (uint32_t)((A.o + A.e - D) * 0x10001), EXTD = (uint32_t)((A.e - D) * 0x10001);
+        // H(r, -1) (Q2), stored at anti-diagonal r - 1
+        auto left = [=](int32_t r) -> uint32_t {
+            return (uint32_t)(pb + D * (r - 1) - (r <= 0 ? 0 : go + ge * r)) * 0x10001u;
+        };
         uint32_t HA[R], HB[R], Ek[R];
         uint32_t dw[GTB ? R : 1];                      // traceback nibbles: last 4 steps per half
 #pragma unroll
@@ -446,26 +459,26 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
                     for (int k = 0; k < R; ++k) dw[k] = 0;   // the window's flags are OR-ed in
                 }
             } else {
-                const uint32_t dtop = (uint32_t)(pb - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
+                // H(-1, c-1) at anti-diagonal c - 2
+                const uint32_t dtop = (uint32_t)(pb + D * (cc - 2) - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
                 if constexpr (GTB)
-                    step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, KK, OEK,
-                                      EXT, NN, j);
+                    step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, OED,
+                                      EXTD, NN, j);
                 else
-                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KK, OEK, EXT,
-                                   NN);
+                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, OED, EXTD, NN);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
                         uint32_t v = 0;
 #pragma unroll
                         for (int k = 0; k < R; ++k) v = (k == (int)kq[h]) ? Hout[k] : v;
-                        score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb;
+                        score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h] - 2);
                     }
                     if (fixable[h] && cc == (int32_t)yl[h] && lg == kp_lane[h]) {
                         uint32_t v = 0;
 #pragma unroll
                         for (int k = 0; k < R; ++k) v = (k == (int)kp[h]) ? Hout[k] : v;
-                        fixv[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb;
+                        fixv[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
                     }
                 }
             }
