@@ -471,6 +471,8 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     // the walk reads one cell per step, mostly from consecutive rows: keep the
     // 16-byte chunk it is in (4 rows of words / 8 rows of 16-bit flags) and the
     // current 8 codes of each sequence, so most steps make no memory access
+    // (loaded once: the CIGAR byte stores may alias any input for the compiler)
+    const uint32_t qoff = A.qoff[tid], toff = pk ? A.toff[tid] : 0u;
     uint4 chunk = make_uint4(0u, 0u, 0u, 0u);
     int64_t chunk_key = -1;
     uint2 qv = make_uint2(0u, 0u), tv = make_uint2(0u, 0u);
@@ -490,8 +492,8 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 const int64_t key = (int64_t)(s >> 2) * q8 + (row & ~7u);
                 if (key != chunk_key) { chunk = *reinterpret_cast<const uint4 *>(tb16 + key); chunk_key = key; }
                 const uint32_t fl = (pick4(chunk, (row & 7u) >> 1) >> (16 * (row & 1u) + (s & 3u))) & 0xFFFFu;
-                const uint32_t qc = tb_code(A.qseq, A.qoff[tid], row, A.seq_packed, qv, qkey);
-                const uint32_t tc = tb_code(A.tseq, A.toff[tid], col, A.seq_packed, tv, tkey);
+                const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
+                const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
                 if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
                 const uint32_t u = fix_diag ? 0u : (fl & 1u);
