@@ -179,9 +179,10 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 // reference's nibble per cell is low2 = (H == tmp) ? (s < 0) : ((H == F) ? 3 : 2),
 // bit2 = E extended, bit3 = F extended; here each cell records four "differs"
 // flags and tb_kernel rebuilds the nibble (s < 0 it takes from the sequences):
-//   u = [H != tmp], w = [H != F], x = [E' != E - e], y = [F' != F - e].
-// A flag is bit 15 of (A + 0x7FFF) - B for A >= B (no carry/borrow crosses a
-// half); v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
+//   u = [H != tmp], w = [H != F], x = [toe > E - e], y = [toe > F - e]
+// (x, y are the reference's own "not extended" tests).  A flag is bit 15 of
+// (A + 0x7FFF) - B: [A != B] for A >= B, [A > B] for |A - B| < 0x7800, and no
+// carry/borrow crosses a half either way; v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
 // v_and_or places them: step j of a 4-step window owns bits j (u), 4+j (w),
 // 8+j (x) and 12+j (y) of each 16-bit half of dw.
 // ---------------------------------------------------------------------------
@@ -205,8 +206,8 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
         const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
         const uint32_t En = pk_max3(toe, em, NN);
         const uint32_t Fn = pk_max3(toe, fm, NN);
-        const uint32_t HC = H + C;
-        const uint32_t fu = HC - tmp, fw = HC - f, fx = (En + C) - em, fy = (Fn + C) - fm;
+        const uint32_t HC = H + C, toeC = toe + C;
+        const uint32_t fu = HC - tmp, fw = HC - f, fx = toeC - em, fy = toeC - fm;
         // bytes: [u, x] per half and [w, y] per half, 0x00 / 0xFF
         const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
         const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
