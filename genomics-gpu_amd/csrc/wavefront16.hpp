@@ -186,7 +186,11 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 // v_and_or places them: step j of a 4-step window owns bits j (u), 4+j (w),
 // 8+j (x) and 12+j (y) of each 16-bit half of dw.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) { return (a & m) | b; }
+// (a & m) | b as one v_bitop3_b32 (truth table 0xEA); the compiler would
+// otherwise split the two merges of a row into and, and, or3
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA);
+}
 
 template <int R>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
