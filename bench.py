@@ -34,6 +34,8 @@ WORKLOADS = {
     # name: (synth kind, default pairs, params, algorithmic bytes per pair, int ops per cell, label)
     "sw_local": (2, 1_000_000, dict(algo=G.LOCAL), 332, 12,
                  "config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp, seed 0x5EED0002"),
+    "sw_local_start": (2, 1_000_000, dict(algo=G.LOCAL, start_pos=G.WITH_START), 340, 12,
+                       "config2 + WITH_START: SW local affine score+ends+starts, 1M pairs x 150bp, seed 0x5EED0002"),
     "nw_tb": (3, 100_000, dict(algo=G.GLOBAL, start_pos=G.WITH_TB), 650, 16,
               "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
     "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
@@ -138,6 +140,8 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
         path = "gasalx_pairhmm_host (pageable host arrays; H2D + kernel + D2H)"
     else:
         fields = ["score"] if params.algo == G.GLOBAL else ["score", "q_end", "t_end"]
+        if params.start_pos == G.WITH_START:
+            fields += ["q_start", "t_start"]
         call = lambda: eng.align_host(data, params, fields=fields)
         path = ("gasalx_align_host (pageable host arrays; chunks of pairs on two streams, "
                 "H2D of chunk k+1 overlapping the kernels of chunk k)")
@@ -199,6 +203,9 @@ def main():
         if pkw["algo"] != G.GLOBAL:
             d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+        if pkw.get("start_pos") == G.WITH_START:
+            d["q_start"] = torch.empty(n, dtype=torch.int32, device=dev)
+            d["t_start"] = torch.empty(n, dtype=torch.int32, device=dev)
         if pkw.get("start_pos") == G.WITH_TB:
             d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
             d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)

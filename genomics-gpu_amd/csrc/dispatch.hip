@@ -9,6 +9,7 @@
 #include "engine.hpp"
 #include "generic.hpp"
 #include "pairhmm.hpp"
+#include "start.hpp"
 #include "wavefront.hpp"
 #include "wavefront16.hpp"
 
@@ -33,7 +34,8 @@ void DevBuf::release() {
     bytes = 0;
 }
 void Workspace::release_all() {
-    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux}) b->release();
+    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
+                      &rev_t, &rev_meta}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -91,7 +93,7 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
 static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
-    if (p.second_best || p.start_pos == 1) return false;
+    if (p.second_best || (p.start_pos == 1 && wf_algo != WF_LOCAL)) return false;
     if (p.start_pos == 2 && wf_algo != WF_GLOBAL) return false;   // packed traceback: GLOBAL only
     // GLOBAL+TB reads the first pad query row, scored -K = -max(b, npen) there:
     // exact for N-vs-base cells only if that equals the reference's -npen
@@ -144,7 +146,11 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     const bool tb = p.start_pos == 2;
     int wf_algo = -1;
     bool keys = false;
-    if (p.algo == 3 /*LOCAL*/ && !p.second_best && p.start_pos != 1) { wf_algo = WF_LOCAL; keys = true; }
+    // LOCAL WITH_START: start.hpp (its reversed query drops pad rows, exact unless N cells score > 0)
+    if (p.algo == 3 /*LOCAL*/ && !p.second_best && !(p.start_pos == 1 && p.has_n_penalty && p.n_penalty < 0)) {
+        wf_algo = WF_LOCAL;
+        keys = true;
+    }
     else if (p.algo == 1 /*GLOBAL*/) { wf_algo = WF_GLOBAL; }
     else if (p.algo == 2 /*SEMI*/ && !p.second_best && p.start_pos != 1) {
         wf_algo = WF_SEMI;
@@ -178,7 +184,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
             if (pl.G16 == 0 || pl.lds16_bytes > 160 * 1024) pl.packed16 = false;
         }
-        const char *an = wf_algo == WF_LOCAL ? "local" : wf_algo == WF_GLOBAL ? "global" : "semi";
+        const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
+                       : wf_algo == WF_GLOBAL ? "global" : "semi";
         if (pl.packed16)
             pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + "_G" + std::to_string(pl.G16) + "R" +
                       std::to_string(pl.R16);
@@ -207,6 +214,110 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     } while (0)
 
 static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
+
+// Launch the wavefront kernel(s) of plan `pl` over one device batch: the packed
+// kernel first when the plan has one (it flags the blocks it aligned), then the
+// int32 kernel, which aligns exactly the pairs of the declined blocks.
+static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &p, const WfArgs &base,
+                            hipStream_t st) {
+    WfArgs A = base;
+    const uint32_t n = A.n;
+    A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
+    A.nval = p.n_code & 0xF;
+    A.has_npen = p.has_n_penalty; A.npen = p.n_penalty;
+    A.head = p.head; A.tail = p.tail;
+    A.lds_stride = pl.lds_stride;
+    A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
+    A.one = 0x00010001u;
+    if (pl.packed16) {
+        // packed kernel first; it marks every block it aligned in ws.misc ...
+        WfArgs P16 = A;
+        P16.lds_stride = pl.lds16_stride;
+        P16.fast16 = 1;
+        P16.vmin = pl.vmin;
+        const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
+        const uint32_t grid16 = grid_for(n, ppb16);
+        HIPCHK(ws.misc.reserve(grid16 + 64));
+        P16.handled = ws.misc.as<uint8_t>();
+        if (pl.tb) {
+            HIPCHK(ws.aux.reserve((size_t)n * 4));
+            P16.tbfix = ws.aux.as<int32_t>();
+        }
+        WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16);
+        if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
+        if (pl.lds16_bytes > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)pl.lds16_bytes));
+        hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
+        HIPCHK(hipGetLastError());
+        // ... and the int32 kernel aligns the pairs of the blocks it declined
+        A.skip = ws.misc.as<uint8_t>();
+        A.skip_ppb = ppb16;
+    }
+    WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+    if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
+    if (pl.lds_bytes > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
+    hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
+    HIPCHK(hipGetLastError());
+    return GASALX_OK;
+}
+
+// LOCAL WITH_START on the wavefront kernels (start.hpp): reversed slots, the
+// same LOCAL kernel over them, and the map of its ends to the start cell.
+static int local_start_reverse(Workspace &ws, const gasalx_params &p, const uint8_t *q, const uint8_t *t,
+                               int packed, const gasalx_batch &b, const BatchShape &shape, const int32_t *score,
+                               const int32_t *qend, const int32_t *tend, int32_t *qstart, int32_t *tstart,
+                               hipStream_t st) {
+    const uint32_t n = b.n_alns;
+    const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t);
+    HIPCHK(ws.rev_q.reserve((size_t)n * q8 + 64));
+    HIPCHK(ws.rev_t.reserve((size_t)n * t8 + 64));
+    const uint32_t t8w = t8 / 8;
+    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 8 + (size_t)t8w * 8 + 64));
+    uint32_t *meta = ws.rev_meta.as<uint32_t>();
+    uint32_t *perm = meta + 7 * (size_t)n, *hist = meta + 8 * (size_t)n, *cursor = hist + t8w;
+    // counting sort of the pairs by reversed target words (longest first)
+    HIPCHK(hipMemsetAsync(hist, 0, (size_t)t8w * 4, st));
+    const size_t sh = (size_t)t8w * 4;
+    if (2 * sh > 64 * 1024) { set_error("LOCAL WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(b.t_lens, tend, n, t8w, hist);
+    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w);
+    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(b.t_lens, tend, n, t8w, cursor, perm);
+    HIPCHK(hipGetLastError());
+    RevArgs R;
+    R.q = q; R.t = t; R.qoff = b.q_offsets; R.toff = b.t_offsets; R.qlen = b.q_lens; R.tlen = b.t_lens;
+    R.qend = qend; R.tend = tend;
+    R.rq = ws.rev_q.as<uint8_t>(); R.rt = ws.rev_t.as<uint8_t>();
+    R.rqoff = meta; R.rtoff = meta + n; R.rqlen = meta + 2 * (size_t)n; R.rtlen = meta + 3 * (size_t)n;
+    R.n = n; R.q8w = q8 / 8; R.t8w = t8w; R.packed = packed;
+    R.fill = 0x01010101u * (uint32_t)(p.n_code & 0xFF);
+    R.nval = (uint32_t)(p.n_code & 0xF);
+    R.perm = perm;
+    const uint64_t items = (uint64_t)n * (R.q8w + R.t8w);
+    rev_prep_kernel<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(R);
+    HIPCHK(hipGetLastError());
+    gasalx_params pr = p;
+    pr.start_pos = 0;
+    BatchShape rs; rs.max_q = q8; rs.max_t = t8;
+    const Plan pl = make_plan(pr, rs, false);
+    if (pl.kind != PLAN_WAVEFRONT) { set_error("reverse pass has no wavefront plan"); return GASALX_EUNSUPPORTED; }
+    int32_t *rscore = reinterpret_cast<int32_t *>(meta + 4 * (size_t)n);
+    int32_t *rqend = rscore + n, *rtend = rscore + 2 * (size_t)n;
+    WfArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.q = R.rq; A.t = R.rt;
+    A.qoff = R.rqoff; A.toff = R.rtoff; A.qlen = R.rqlen; A.tlen = R.rtlen;
+    A.score = rscore; A.qend = rqend; A.tend = rtend;
+    A.n = n;
+    A.packed = 0;
+    int rc = launch_wavefront(ws, pl, pr, A, st);
+    if (rc) return rc;
+    start_map_kernel<<<grid_for(n, 256), 256, 0, st>>>(perm, score, R.rqlen, b.t_lens, tend, rqend, rtend, qstart,
+                                                        tstart, n);
+    HIPCHK(hipGetLastError());
+    return GASALX_OK;
+}
 
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
                  hipStream_t st, const BatchShape &shape, uint64_t cigar_cap) {
@@ -264,8 +375,9 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     if (pl.packed16 && pl.tb)
         tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pad8(shape.max_q) * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
     int32_t *qend = out.q_end, *tend = out.t_end;
-    if (runs_tb) {
-        HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
+    const bool local_start = pl.kind == PLAN_WAVEFRONT && p.algo == 3 && p.start_pos == 1 && (out.q_start || out.t_start);
+    if (runs_tb) HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
+    if (runs_tb || local_start) {
         if (p.algo == 3 && (!qend || !tend)) {
             HIPCHK(ws.ends_q.reserve((size_t)n * 4));
             HIPCHK(ws.ends_t.reserve((size_t)n * 4));
@@ -285,45 +397,18 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.tb = ws.tb.as<uint32_t>();
         A.tb_pair_words = tb_words;
         A.n = n;
-        A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
-        A.nval = p.n_code & 0xF;
-        A.has_npen = p.has_n_penalty; A.npen = p.n_penalty;
-        A.head = p.head; A.tail = p.tail;
         A.packed = packed;
-        A.lds_stride = pl.lds_stride;
-        A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
-        A.one = 0x00010001u;
-        if (pl.packed16) {
-            // packed kernel first; it marks every block it aligned in ws.misc ...
-            WfArgs P16 = A;
-            P16.lds_stride = pl.lds16_stride;
-            P16.fast16 = 1;
-            P16.vmin = pl.vmin;
-            const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
-            const uint32_t grid16 = grid_for(n, ppb16);
-            HIPCHK(ws.misc.reserve(grid16 + 64));
-            P16.handled = ws.misc.as<uint8_t>();
-            if (pl.tb) {
-                HIPCHK(ws.aux.reserve((size_t)n * 4));
-                P16.tbfix = ws.aux.as<int32_t>();
+        int rc = launch_wavefront(ws, pl, p, A, st);
+        if (rc) return rc;
+        if (local_start) {
+            if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {
+                set_error("LOCAL WITH_START: batch too large for one call (reversed slots exceed 4 GB)");
+                return GASALX_ERANGE;
             }
-            WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16);
-            if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
-            if (pl.lds16_bytes > 64 * 1024)
-                HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)pl.lds16_bytes));
-            hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
-            HIPCHK(hipGetLastError());
-            // ... and the int32 kernel aligns the pairs of the blocks it declined
-            A.skip = ws.misc.as<uint8_t>();
-            A.skip_ppb = ppb16;
+            rc = local_start_reverse(ws, p, qsrc, tsrc, packed, b, shape, out.aln_score, qend, tend, out.q_start,
+                                     out.t_start, st);
+            if (rc) return rc;
         }
-        WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
-        if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
-        if (pl.lds_bytes > 64 * 1024)
-            HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
-        hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
-        HIPCHK(hipGetLastError());
     } else {
         GenArgs A;
         std::memset(&A, 0, sizeof(A));

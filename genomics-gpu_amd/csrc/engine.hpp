@@ -31,6 +31,7 @@ struct Workspace {
     DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
     DevBuf misc;                    // packed kernels: per-block "aligned here" flags
     DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
+    DevBuf rev_q, rev_t, rev_meta;  // LOCAL WITH_START: reversed slots, their offsets/lengths, reverse results
     void release_all();
 };
 

@@ -117,6 +117,59 @@ def test_local_with_start(engine):
     check(engine, G.Batch.from_pairs(q, t), algo=G.LOCAL, start_pos=G.WITH_START)
 
 
+@pytest.mark.parametrize("qr,tr,alphabet,scores", [
+    ((1, 40), (1, 40), b"ACGT", (1, 4, 6, 1)),
+    ((140, 160), (140, 160), b"ACGT", (1, 4, 6, 1)),
+    ((1, 200), (1, 250), b"ACGTN", (1, 4, 6, 1)),
+    ((50, 150), (50, 180), b"ACGTRYacgt", (1, 4, 6, 1)),       # declined blocks -> int32 kernel both passes
+    ((60, 160), (60, 160), b"ACGT", (2, 3, 5, 2)),
+    ((60, 160), (60, 160), b"ACGT", (3, 6, 0, 0)),
+    ((200, 320), (150, 400), b"ACGT", (1, 4, 6, 1)),          # int32 wavefront (target > 256)
+])
+def test_local_with_start_wavefront(engine, qr, tr, alphabet, scores):
+    # WITH_START runs the LOCAL wavefront kernel twice (forward, then on the reversed
+    # end-word-aligned slots, start.hpp); local_kernel_template.h:441-511 incl. Q8
+    a, bb, o, e = scores
+    kw = dict(algo=G.LOCAL, start_pos=G.WITH_START, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+    assert G.describe_plan(G.make_params(**kw), qr[1], tr[1]).startswith(("wavefront16_local_start",
+                                                                            "wavefront_local_start"))
+    b = rand_batch(zlib.crc32(repr((qr, tr, alphabet, scores)).encode()) & 0xFFFF, 1200, *qr, *tr,
+                   alphabet=alphabet, related=0.5)
+    check(engine, b, **kw)
+
+
+def test_local_with_start_config2_sample(engine):
+    check(engine, G.Batch.synth(2, 20000, 0x5EED0002), algo=G.LOCAL, start_pos=G.WITH_START)
+
+
+def test_local_with_start_shared_query_and_zero_scores(engine):
+    # one-to-many pairing (every pair reads the same query slot) and all-mismatch pairs (score 0 -> start 0,0)
+    rng = np.random.default_rng(77)
+    q = helpers.random_seq(rng, 120, b"ACGT")
+    ts = [helpers.random_seq(rng, int(rng.integers(1, 200)), b"ACGT") for _ in range(300)] + [b"TTTT"] * 5
+    b1 = G.Batch.from_pairs([q] * len(ts), ts)
+    shared = G.Batch(b1.q_data[:int(b1.q_offsets[1])].copy(), np.zeros(b1.n, np.uint32), b1.q_lens,
+                     b1.t_data, b1.t_offsets, b1.t_lens)
+    check(engine, shared, algo=G.LOCAL, start_pos=G.WITH_START)
+    zb = G.Batch.from_pairs([b"AAAA", b"A", b"CCCCCCCCC"], [b"TTTT", b"G", b"GGG"])
+    g, _ = check(engine, zb, algo=G.LOCAL, start_pos=G.WITH_START)
+    assert list(g["q_start"]) == [0, 0, 0] and list(g["t_start"]) == [0, 0, 0]
+
+
+@pytest.mark.parametrize("npen", [0, 2, -1])
+def test_local_with_start_n_penalty(engine, npen):
+    b = rand_batch(98 + npen, 800, 5, 150, 5, 170, alphabet=b"ACGTACGTN", related=0.6)
+    check(engine, b, algo=G.LOCAL, start_pos=G.WITH_START, n_penalty=npen)
+
+
+def test_local_with_start_packed_and_ops(engine):
+    b = rand_batch(96, 600, 10, 150, 10, 150)
+    rng = np.random.default_rng(97)
+    qo = rng.integers(0, 4, b.n).astype(np.uint8)
+    to = rng.integers(0, 4, b.n).astype(np.uint8)
+    check(engine, b, q_ops=qo, t_ops=to, algo=G.LOCAL, start_pos=G.WITH_START)
+
+
 def test_local_second_best(engine):
     check(engine, rand_batch(22, 600, 30, 150, 30, 200), algo=G.LOCAL, second_best=1)
 
