@@ -40,6 +40,10 @@ WORKLOADS = {
               "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
     "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
              "config4 shard: semi-global TARGET/TARGET, 150bp reads in 182bp windows, seed 0x5EED0004"),
+    "semi_start": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
+                                      max_query_len=192), 372, 12,
+                   "config4 shard + WITH_START: semi-global TARGET/TARGET score+ends+starts, 150bp reads in 182bp "
+                   "windows, seed 0x5EED0004"),
     "pairhmm": (5, 100_000, None, 4762, 11,
                 "config5: PairHMM fp32 forward, 100K reads x haplotypes (250 x 500), seed 0x5EED0005"),
 }

@@ -58,6 +58,14 @@ static WfFn wf_pick(int G, int R) {
     return nullptr;
 }
 
+static WfFn wf_pick_stop(int G, int R) {   // SEMI TAIL=TARGET reverse pass (start.hpp)
+#define GX_CASE(g, r) if (G == g && R == r) return &wf_kernel<WF_SEMI, true, false, g, r, true>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
 static WfFn wf_lookup(int algo, bool keys, bool tb, int G, int R) {
     if (algo == WF_LOCAL) return tb ? wf_pick<WF_LOCAL, true, true>(G, R) : wf_pick<WF_LOCAL, true, false>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf_pick<WF_GLOBAL, false, true>(G, R) : wf_pick<WF_GLOBAL, false, false>(G, R);
@@ -93,7 +101,7 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
 static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
-    if (p.second_best || (p.start_pos == 1 && wf_algo != WF_LOCAL)) return false;
+    if (p.second_best || (p.start_pos == 1 && wf_algo == WF_GLOBAL)) return false;
     if (p.start_pos == 2 && wf_algo != WF_GLOBAL) return false;   // packed traceback: GLOBAL only
     // GLOBAL+TB reads the first pad query row, scored -K = -max(b, npen) there:
     // exact for N-vs-base cells only if that equals the reference's -npen
@@ -152,11 +160,12 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         keys = true;
     }
     else if (p.algo == 1 /*GLOBAL*/) { wf_algo = WF_GLOBAL; }
-    else if (p.algo == 2 /*SEMI*/ && !p.second_best && p.start_pos != 1) {
+    else if (p.algo == 2 /*SEMI*/ && !p.second_best && (p.start_pos != 1 || p.tail == 2)) {   // WITH_START: start.hpp
         wf_algo = WF_SEMI;
         keys = (p.tail == 2 || p.tail == 3);
     }
     bool ok = wf_algo >= 0 && int16_safe(p, s.max_q, s.max_t) && t8 < 32000 && p.gap_extend >= 0;
+    if (wf_algo == WF_SEMI && p.start_pos == 1 && t8 > 8192) ok = false;   // stop key: strips < 1024
     if (ok) {
         const Shape *pick = nullptr;
         for (const Shape &sh : kShapes)
@@ -185,7 +194,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             if (pl.G16 == 0 || pl.lds16_bytes > 160 * 1024) pl.packed16 = false;
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
-                       : wf_algo == WF_GLOBAL ? "global" : "semi";
+                       : wf_algo == WF_GLOBAL ? "global" : (p.start_pos == 1 ? "semi_start" : "semi");
         if (pl.packed16)
             pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + "_G" + std::to_string(pl.G16) + "R" +
                       std::to_string(pl.R16);
@@ -254,7 +263,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         A.skip = ws.misc.as<uint8_t>();
         A.skip_ppb = ppb16;
     }
-    WfFn fn = wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+    WfFn fn = A.stop ? wf_pick_stop(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
     if (pl.lds_bytes > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
@@ -263,34 +272,38 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
     return GASALX_OK;
 }
 
-// LOCAL WITH_START on the wavefront kernels (start.hpp): reversed slots, the
-// same LOCAL kernel over them, and the map of its ends to the start cell.
-static int local_start_reverse(Workspace &ws, const gasalx_params &p, const uint8_t *q, const uint8_t *t,
-                               int packed, const gasalx_batch &b, const BatchShape &shape, const int32_t *score,
-                               const int32_t *qend, const int32_t *tend, int32_t *qstart, int32_t *tstart,
-                               hipStream_t st) {
+// WITH_START on the wavefront kernels (start.hpp): reversed slots sorted by
+// reversed target length, the same kernel over them, and the map of its ends to
+// the start cell.
+static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const uint8_t *q, const uint8_t *t,
+                         int packed, const gasalx_batch &b, const BatchShape &shape, const int32_t *score,
+                         const int32_t *qend, const int32_t *tend, int32_t *qstart, int32_t *tstart, hipStream_t st) {
     const uint32_t n = b.n_alns;
-    const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t);
+    const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t), t8w = t8 / 8;
     HIPCHK(ws.rev_q.reserve((size_t)n * q8 + 64));
     HIPCHK(ws.rev_t.reserve((size_t)n * t8 + 64));
-    const uint32_t t8w = t8 / 8;
-    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 8 + (size_t)t8w * 8 + 64));
+    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 9 + (size_t)(t8w + 1) * 8 + 64));
     uint32_t *meta = ws.rev_meta.as<uint32_t>();
-    uint32_t *perm = meta + 7 * (size_t)n, *hist = meta + 8 * (size_t)n, *cursor = hist + t8w;
+    int32_t *rscore = reinterpret_cast<int32_t *>(meta + 4 * (size_t)n);
+    int32_t *rqend = rscore + n, *rtend = rscore + 2 * (size_t)n;
+    uint32_t *perm = meta + 7 * (size_t)n;
+    int32_t *stop = reinterpret_cast<int32_t *>(meta + 8 * (size_t)n);
+    uint32_t *hist = meta + 9 * (size_t)n, *cursor = hist + t8w + 1;
     // counting sort of the pairs by reversed target words (longest first)
-    HIPCHK(hipMemsetAsync(hist, 0, (size_t)t8w * 4, st));
-    const size_t sh = (size_t)t8w * 4;
-    if (2 * sh > 64 * 1024) { set_error("LOCAL WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(b.t_lens, tend, n, t8w, hist);
-    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w);
-    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(b.t_lens, tend, n, t8w, cursor, perm);
+    const size_t sh = (size_t)(t8w + 1) * 4;
+    if (2 * sh > 64 * 1024) { set_error("WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
+    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist);
+    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
+    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm);
     HIPCHK(hipGetLastError());
     RevArgs R;
     R.q = q; R.t = t; R.qoff = b.q_offsets; R.toff = b.t_offsets; R.qlen = b.q_lens; R.tlen = b.t_lens;
-    R.qend = qend; R.tend = tend;
+    R.qend = qend; R.tend = tend; R.score = score;
     R.rq = ws.rev_q.as<uint8_t>(); R.rt = ws.rev_t.as<uint8_t>();
     R.rqoff = meta; R.rtoff = meta + n; R.rqlen = meta + 2 * (size_t)n; R.rtlen = meta + 3 * (size_t)n;
-    R.n = n; R.q8w = q8 / 8; R.t8w = t8w; R.packed = packed;
+    R.stop = mode == REV_SEMI ? stop : nullptr;
+    R.n = n; R.q8w = q8 / 8; R.t8w = t8w; R.packed = packed; R.mode = mode;
     R.fill = 0x01010101u * (uint32_t)(p.n_code & 0xFF);
     R.nval = (uint32_t)(p.n_code & 0xF);
     R.perm = perm;
@@ -302,19 +315,18 @@ static int local_start_reverse(Workspace &ws, const gasalx_params &p, const uint
     BatchShape rs; rs.max_q = q8; rs.max_t = t8;
     const Plan pl = make_plan(pr, rs, false);
     if (pl.kind != PLAN_WAVEFRONT) { set_error("reverse pass has no wavefront plan"); return GASALX_EUNSUPPORTED; }
-    int32_t *rscore = reinterpret_cast<int32_t *>(meta + 4 * (size_t)n);
-    int32_t *rqend = rscore + n, *rtend = rscore + 2 * (size_t)n;
     WfArgs A;
     std::memset(&A, 0, sizeof(A));
     A.q = R.rq; A.t = R.rt;
     A.qoff = R.rqoff; A.toff = R.rtoff; A.qlen = R.rqlen; A.tlen = R.rtlen;
     A.score = rscore; A.qend = rqend; A.tend = rtend;
+    A.stop = R.stop;
     A.n = n;
     A.packed = 0;
     int rc = launch_wavefront(ws, pl, pr, A, st);
     if (rc) return rc;
-    start_map_kernel<<<grid_for(n, 256), 256, 0, st>>>(perm, score, R.rqlen, b.t_lens, tend, rqend, rtend, qstart,
-                                                        tstart, n);
+    start_map_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, perm, score, b.q_lens, R.rqlen, b.t_lens, tend, rscore,
+                                                        rqend, rtend, qstart, tstart, n);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }
@@ -375,10 +387,11 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     if (pl.packed16 && pl.tb)
         tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pad8(shape.max_q) * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
     int32_t *qend = out.q_end, *tend = out.t_end;
-    const bool local_start = pl.kind == PLAN_WAVEFRONT && p.algo == 3 && p.start_pos == 1 && (out.q_start || out.t_start);
+    const bool wf_start = pl.kind == PLAN_WAVEFRONT && (p.algo == 3 || p.algo == 2) && p.start_pos == 1 &&
+                          (out.q_start || out.t_start);
     if (runs_tb) HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
-    if (runs_tb || local_start) {
-        if (p.algo == 3 && (!qend || !tend)) {
+    if (runs_tb || wf_start) {
+        if ((p.algo == 3 || p.algo == 2) && (!qend || !tend)) {
             HIPCHK(ws.ends_q.reserve((size_t)n * 4));
             HIPCHK(ws.ends_t.reserve((size_t)n * 4));
             if (!qend) qend = ws.ends_q.as<int32_t>();
@@ -400,13 +413,13 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.packed = packed;
         int rc = launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
-        if (local_start) {
+        if (wf_start) {
             if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {
-                set_error("LOCAL WITH_START: batch too large for one call (reversed slots exceed 4 GB)");
+                set_error("WITH_START: batch too large for one call (reversed slots exceed 4 GB)");
                 return GASALX_ERANGE;
             }
-            rc = local_start_reverse(ws, p, qsrc, tsrc, packed, b, shape, out.aln_score, qend, tend, out.q_start,
-                                     out.t_start, st);
+            rc = start_reverse(ws, p.algo == 3 ? REV_LOCAL : REV_SEMI, p, qsrc, tsrc, packed, b, shape, out.aln_score,
+                               qend, tend, out.q_start, out.t_start, st);
             if (rc) return rc;
         }
     } else {

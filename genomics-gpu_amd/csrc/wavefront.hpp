@@ -47,6 +47,9 @@ struct WfArgs {
     const uint8_t *skip;       // int32 kernel: pairs whose packed block already aligned them
     uint32_t skip_ppb;         // pairs per packed block
     int32_t *tbfix;            // wavefront16 GLOBAL+TB: H at the traceback start cell (ql, tl), see tb_kernel
+    const int32_t *stop;       // SEMI TAIL=TARGET reverse pass (start.hpp): per pair, the forward score; the
+                               // last-row maximum is then taken inside the first 8-column strip holding a
+                               // value >= it (the reference's early exit), else over the whole row
 
 };
 
@@ -87,7 +90,7 @@ __device__ __forceinline__ uint32_t load4_codes(const uint8_t *base, uint32_t of
            ((half & 15u) << 24);
 }
 
-template <int ALGO, bool KEYS, bool TB, int G, int R, bool EXACT>
+template <int ALGO, bool KEYS, bool TB, int G, int R, bool EXACT, bool STOP>
 __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, const uint32_t lg,
                                         const uint32_t pair, const bool valid, const uint32_t ql,
                                         const uint32_t tl, const uint32_t qpad, const uint32_t tpad,
@@ -132,6 +135,7 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
 
     const uint32_t kq_lane = (ql - 1) / R;      // lane holding the last query row
     const uint32_t kq = (ql - 1) - kq_lane * R;
+    const int32_t thr = (STOP && valid) ? A.stop[pair] : 0;
 
     for (uint32_t s = 0; s < nsteps; ++s) {
         const int32_t c = (int32_t)s - (int32_t)lg;
@@ -184,7 +188,15 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
                     diag = Hk[k];
                     Hk[k] = H - OE;
                     f = max(Hk[k], f - ext);                             // F(r+1,c)
-                    if (KEYS) key[k] = max(key[k], H * 32768 + Cc);
+                    if (STOP) {
+                        // cells >= thr rank first: smallest strip, then largest H, then first
+                        // column; the others by (H, first column); columns >= tl never
+                        const int32_t kv = (uint32_t)c >= tl ? INT32_MIN
+                                         : H >= thr ? (0x40000000 | ((1023 - (c >> 3)) << 19) | ((H - thr) << 3) |
+                                                       (7 - (c & 7)))
+                                                    : H * 16384 + (16383 - c);
+                        key[k] = max(key[k], kv);
+                    } else if (KEYS) key[k] = max(key[k], H * 32768 + Cc);
                 } else {
                     // CORE_LOCAL_COMPUTE / CORE_GLOBAL_COMPUTE (local :19-30, global.h:4-12)
                     const int32_t tmp = diag + sc;
@@ -269,7 +281,8 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
             int32_t kk = INT32_MIN;
 #pragma unroll
             for (int k = 0; k < R; ++k) kk = (k == (int)kq) ? key[k] : kk;
-            if (kk >= 0) bt = ((uint64_t)(uint32_t)kk) | (1ull << 40);
+            if (STOP) { if (kk != INT32_MIN) bt = (uint64_t)((uint32_t)kk ^ 0x80000000u) | (1ull << 40); }
+            else if (kk >= 0) bt = ((uint64_t)(uint32_t)kk) | (1ull << 40);
         }
         // TAIL QUERY: H at the last padded column, rows < ql, first max (:185-193)
         uint64_t bq = 0;
@@ -288,7 +301,18 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
         bq = group_max_u64<G>(bq);
         if (valid && lg == 0) {
             int32_t maxHH = -32768, maxX = (int32_t)tl, maxY = (int32_t)ql;   // :49,63-64 (Q10)
-            if (tail_t && bt != 0) {
+            if (STOP && bt != 0) {
+                const int32_t kk = (int32_t)((uint32_t)bt ^ 0x80000000u);
+                int32_t H, col;
+                if (kk >= 0x40000000) {
+                    col = 8 * (1023 - ((kk >> 19) & 1023)) + 7 - (kk & 7);
+                    H = thr + ((kk >> 3) & 0xFFFF);
+                } else {
+                    H = kk >> 14;                                   // floor: 16383 - c in [0, 16384)
+                    col = 16383 - (kk & 16383);
+                }
+                maxHH = H; maxY = col;
+            } else if (tail_t && bt != 0) {
                 const uint32_t kk = (uint32_t)bt;
                 const int32_t H = (int32_t)(kk >> 15) - 32768;
                 const int32_t col = 32767 - (int32_t)(kk & 0x7FFFu);
@@ -309,7 +333,7 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
     }
 }
 
-template <int ALGO, bool KEYS, bool TB, int G, int R>
+template <int ALGO, bool KEYS, bool TB, int G, int R, bool STOP = false>
 __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int P = 64 / G;
@@ -373,9 +397,9 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     bool exact = A.force_exact != 0;
     if (ALGO != WF_GLOBAL || A.has_npen) exact = exact || __any(has_n);
     if (exact)
-        wf_body<ALGO, KEYS, TB, G, R, true>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+        wf_body<ALGO, KEYS, TB, G, R, true, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
     else
-        wf_body<ALGO, KEYS, TB, G, R, false>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+        wf_body<ALGO, KEYS, TB, G, R, false, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
 }
 
 }  // namespace gx

@@ -563,8 +563,16 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
         reset(HA);
 #pragma unroll
         for (int k = 0; k < R; ++k) HB[k] = HA[k];
-        // TAIL=TARGET: max over the last query row, columns < tl, first (smallest) column
+        // TAIL=TARGET: max over the last query row, columns < tl, first (smallest) column.
+        // Reverse pass (A.stop, start.hpp): values >= the forward score rank first,
+        // by smallest 8-column strip, then value, then first column (bit 31 set).
         uint32_t best[2] = {0, 0};
+        int32_t thrp[2] = {0x7FFFFFFF, 0x7FFFFFFF};
+        if (A.stop) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (valid[h]) thrp[h] = A.stop[pr[h]] + pb - oe;   // stored pattern of the forward score
+        }
         uint32_t recvH = HA[R - 1], prevRecvH = HA[R - 1], recvE = NN, hl = 0, el = 0;
         uint2 tnext = tcol[c + G];
         auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
@@ -583,7 +591,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
                         for (int k = 0; k < R; ++k) {
                             const uint32_t col = r0 + k;
                             const uint32_t v = (Hout[k] >> (16 * h)) & 0xFFFFu;
-                            const uint32_t cand = col < xl[h] ? (v << 16) | (0xFFFFu - col) : 0u;
+                            const uint32_t cand =
+                                col >= xl[h] ? 0u
+                                : (int32_t)v >= thrp[h]
+                                    ? 0x80000000u | ((255u - (col >> 3)) << 23) | (v << 8) | (255u - (col & 7u))
+                                    : (v << 16) | (0xFFFFu - col);
                             best[h] = cand > best[h] ? cand : best[h];
                         }
                     }
@@ -605,7 +617,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
             if (valid[h] && lg == 0) {
                 // semiglobal :49,63-64,206-218 (Q10): q_end = tl, t_end = column of the max
                 int32_t score = -32768, qe = (int32_t)xl[h], te = (int32_t)yl[h];
-                if (b != 0) {
+                if (b & 0x80000000u) {
+                    score = (int32_t)((b >> 8) & 0x7FFFu) - pb + oe;
+                    te = (int32_t)(8 * (255u - ((b >> 23) & 255u)) + (255u - (b & 255u)));
+                } else if (b != 0) {
                     score = (int32_t)(b >> 16) - pb + oe;
                     te = (int32_t)(0xFFFFu - (b & 0xFFFFu));
                 }

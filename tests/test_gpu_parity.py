@@ -225,6 +225,33 @@ def test_semiglobal_with_start(engine, head, tail):
     check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, start_pos=G.WITH_START, max_query_len=160)
 
 
+@pytest.mark.parametrize("head", [G.NONE, G.QUERY, G.TARGET, G.BOTH])
+@pytest.mark.parametrize("alphabet,scores", [(b"ACGT", (1, 4, 6, 1)), (b"ACGTN", (1, 4, 6, 1)),
+                                             (b"ACGTRYacgt", (1, 4, 6, 1)),      # declined -> int32 stop kernel
+                                             (b"ACGT", (2, 3, 5, 2)), (b"ACGT", (3, 6, 0, 0))])
+def test_semiglobal_with_start_wavefront(engine, head, alphabet, scores):
+    # TAIL=TARGET WITH_START: reverse pass = the same kernel on reversed slots with the
+    # early-exit stop key (start.hpp; semiglobal_kernel_template.h:227-383)
+    a, bb, o, e = scores
+    kw = dict(algo=G.SEMI_GLOBAL, head=head, tail=G.TARGET, start_pos=G.WITH_START, match=a, mismatch=bb,
+              gap_open=o, gap_extend=e, max_query_len=512)
+    assert G.describe_plan(G.make_params(**kw), 200, 260).startswith(("wavefront16_semi_start", "wavefront_semi_start"))
+    b = rand_batch(zlib.crc32(repr((head, alphabet, scores)).encode()) & 0xFFFF, 1000, 1, 200, 1, 260,
+                   alphabet=alphabet, related=0.6)
+    check(engine, b, **kw)
+
+
+def test_semiglobal_with_start_reads_in_windows(engine):
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START, max_query_len=192)
+    check(engine, G.Batch.synth(4, 20000, 0x5EED0004), **kw)
+    for n in (1, 7, 33):
+        check(engine, rand_batch(500 + n, n, 1, 150, 1, 190), **kw)
+    b = rand_batch(510, 500, 10, 150, 10, 150)
+    rng = np.random.default_rng(511)
+    check(engine, b, q_ops=rng.integers(0, 4, b.n).astype(np.uint8), t_ops=rng.integers(0, 4, b.n).astype(np.uint8),
+          **kw)
+
+
 def test_semiglobal_reads_in_windows(engine):
     b = G.Batch.synth(4, 2000, 0x5EED0004)
     check(engine, b, algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET)
