@@ -36,6 +36,8 @@ WORKLOADS = {
                  "config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp, seed 0x5EED0002"),
     "sw_local_start": (2, 1_000_000, dict(algo=G.LOCAL, start_pos=G.WITH_START), 340, 12,
                        "config2 + WITH_START: SW local affine score+ends+starts, 1M pairs x 150bp, seed 0x5EED0002"),
+    "sw_local_tb": (2, 1_000_000, dict(algo=G.LOCAL, start_pos=G.WITH_TB), 340 + 152, 16,
+                    "config2 + WITH_TB: SW local affine score+ends+starts+CIGAR, 1M pairs x 150bp, seed 0x5EED0002"),
     "nw_tb": (3, 100_000, dict(algo=G.GLOBAL, start_pos=G.WITH_TB), 650, 16,
               "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
     "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
@@ -207,7 +209,7 @@ def main():
         if pkw["algo"] != G.GLOBAL:
             d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
-        if pkw.get("start_pos") == G.WITH_START:
+        if pkw.get("start_pos") in (G.WITH_START, G.WITH_TB) and pkw["algo"] != G.GLOBAL:
             d["q_start"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_start"] = torch.empty(n, dtype=torch.int32, device=dev)
         if pkw.get("start_pos") == G.WITH_TB:

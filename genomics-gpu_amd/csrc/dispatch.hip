@@ -89,8 +89,16 @@ static WfFn wf16_pick_tb(int G, int R) {   // R % 4 == 0 shapes (wavefront16.hpp
     return nullptr;
 }
 
+static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
+#define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<WF16_LOCAL_TB, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
 static WfFn wf16_lookup(int algo, bool tb, int G, int R) {
-    if (algo == WF_LOCAL) return wf16_pick<WF_LOCAL>(G, R);
+    if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return wf16_pick<WF_SEMI>(G, R);
 }
@@ -102,10 +110,10 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
 static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
     if (p.second_best || (p.start_pos == 1 && wf_algo == WF_GLOBAL)) return false;
-    if (p.start_pos == 2 && wf_algo != WF_GLOBAL) return false;   // packed traceback: GLOBAL only
+    if (p.start_pos == 2 && wf_algo == WF_SEMI) return false;     // no traceback for SEMI (reference)
     // GLOBAL+TB reads the first pad query row, scored -K = -max(b, npen) there:
     // exact for N-vs-base cells only if that equals the reference's -npen
-    if (p.start_pos == 2 && p.has_n_penalty && p.n_penalty < p.mismatch) return false;
+    if (p.start_pos == 2 && wf_algo == WF_GLOBAL && p.has_n_penalty && p.n_penalty < p.mismatch) return false;
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
     const int64_t a = p.match, b = p.mismatch, oe = (int64_t)p.gap_open + p.gap_extend, e = p.gap_extend;

@@ -496,6 +496,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
                 if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
+                if (A.is_local && !A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = 0;   // local N rule
                 const uint32_t u = fix_diag ? 0u : (fl & 1u);
                 fix_diag = false;
                 cell_op = (u ? ((fl & 16u) ? 2u : 3u) : (sc < 0 ? 1u : 0u)) | ((fl & 256u) ? 0u : 4u) |

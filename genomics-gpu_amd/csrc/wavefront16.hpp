@@ -80,6 +80,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
+#ifndef GX_WF16_LTB_WAVES
+#define GX_WF16_LTB_WAVES 2   // LOCAL + traceback kernel
+#endif
 
 // A/C/G/T nibble -> 0..3, N -> 4, anything else -> 5
 __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
@@ -228,6 +231,50 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
 }
 
 // ---------------------------------------------------------------------------
+// LOCAL step with traceback flags (local_kernel_template.h:45-60 nibbles): the
+// LOCAL update of step_local plus the four "differs" flags of step_global_tb.
+// E and F are floored at 0 here (the reference's are not); on every cell the
+// walk visits (H > 0, gap values > 0, get_tb.h:100-103 stops before H = 0)
+// the flags agree: u = [H != tmp] is unchanged, w = [H != F] differs only
+// where H = 0, x/y only where the floored value's successor is <= 0.
+// ---------------------------------------------------------------------------
+template <int R>
+__device__ __forceinline__ void step_local_tb(const uint2 T, const int32_t c, const uint32_t diag_top,
+                                              const uint32_t f_top, const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
+                                              uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
+                                              uint32_t (&dw)[R], uint32_t &f_out, const uint32_t KK,
+                                              const uint32_t OEK, const uint32_t EXT, const uint32_t BB,
+                                              const uint32_t KMUL, const uint32_t bshift, const int j) {
+    constexpr uint32_t C = 0x7FFF7FFFu;
+    const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
+    const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
+    const uint32_t invc = ((col - bshift) & 0xFFFFu) * 0x10001u;   // key = H*256 + col (mod 2^16)
+    uint32_t diag = diag_top, f = f_top;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KK);
+        const uint32_t toe = pk_subnb(t1, OEK);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
+        const uint32_t En = pk_max3(toe, em, BB);
+        const uint32_t Fn = pk_max3(toe, fm, BB);
+        key[k] = pk_max_u16(key[k], pk_mad_u16(H, KMUL, invc));
+        const uint32_t HC = H + C, toeC = toe + C;
+        const uint32_t fu = HC - tmp, fw = HC - f, fx = toeC - em, fy = toeC - fm;
+        const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
+        const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
+        dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
+        Ek[k] = En;
+        f = Fn;
+        diag = Hin[k];
+        Hout[k] = H;
+    }
+    f_out = f;
+}
+
+// ---------------------------------------------------------------------------
 // SEMI step (transposed): registers = target columns, one query row per step.
 // Stored values are H - OE ("Hm").  In: diag_top = Hm(r-1, c0-1),
 // hl/el = Hm(r, c0-1) / E(r, c0-1) entering the lane's first column.
@@ -255,12 +302,15 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 // The kernel.
 // ---------------------------------------------------------------------------
 constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
+constexpr int WF16_LOCAL_TB = 4;      // LOCAL with traceback words (wavefront16 only)
 
 template <int ALGO_, int G, int R>
-__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
+__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
+                                   : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
-    constexpr int ALGO = GTB ? WF_GLOBAL : ALGO_;
+    constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
+    constexpr int ALGO = GTB ? WF_GLOBAL : LTB ? WF_LOCAL : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -371,21 +421,62 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES 
         for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
         uint32_t recvH = BB, prevRecvH = BB, recvF = BB, f = BB;
         uint2 tnext = tcol[c + G];
-        for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-            uint2 T = tnext;
-            tnext = tcol[c + 1 + G];
-            step_local<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, f, KK, OEK, EXT, BB,
-                          KMUL, bshift);
-            prevRecvH = recvH;
-            recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
-            recvF = (uint32_t)shr_lane((int32_t)f);
-            T = tnext;
-            tnext = tcol[c + 2 + G];
-            step_local<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, f, KK, OEK, EXT,
-                          BB, KMUL, bshift);
-            prevRecvH = recvH;
-            recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
-            recvF = (uint32_t)shr_lane((int32_t)f);
+        if constexpr (LTB) {
+            // direction flags in the skewed layout of the GLOBAL+TB kernel (see there)
+            static_assert(R % 4 == 0, "LOCAL+TB packed shapes need R % 4 == 0");
+            uint32_t dw[R];
+#pragma unroll
+            for (int k = 0; k < R; ++k) dw[k] = 0;
+            uint32_t W16[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
+            auto qstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+                const uint2 T = tnext;
+                tnext = tcol[c + j + 1 + G];
+                step_local_tb<R>(T, c + j, top ? BB : prevRecvH, top ? BB : recvF, xs, Hin, Hout, Ek, key, dw, f, KK,
+                                 OEK, EXT, BB, KMUL, bshift, j);
+                prevRecvH = recvH;
+                recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
+                recvF = (uint32_t)shr_lane((int32_t)f);
+            };
+            for (uint32_t s = 0; s < nsteps; s += 4, c += 4) {
+                qstep(0, HA, HB);
+                qstep(1, HB, HA);
+                qstep(2, HA, HB);
+                qstep(3, HB, HA);
+                const uint32_t w = s >> 2;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (valid[h] && w < W16[h]) {
+                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                                        (uint64_t)w * xpad[h] + r0;
+                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+                        for (int k = 0; k < R; k += 4)
+                            if (r0 + k < xpad[h])
+                                *reinterpret_cast<uint2 *>(dst + k) =
+                                    make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
+                                               __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+                    }
+                }
+            }
+        } else {
+            for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
+                uint2 T = tnext;
+                tnext = tcol[c + 1 + G];
+                step_local<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, f, KK, OEK, EXT, BB,
+                              KMUL, bshift);
+                prevRecvH = recvH;
+                recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
+                recvF = (uint32_t)shr_lane((int32_t)f);
+                T = tnext;
+                tnext = tcol[c + 2 + G];
+                step_local<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, f, KK, OEK, EXT,
+                              BB, KMUL, bshift);
+                prevRecvH = recvH;
+                recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
+                recvF = (uint32_t)shr_lane((int32_t)f);
+            }
         }
         // ---- strip-major first maximum per pair (Q1) ----
 #pragma unroll

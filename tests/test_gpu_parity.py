@@ -429,6 +429,25 @@ def test_packed_global_traceback(engine, scores, alphabet):
     check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
 
 
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2), (1, 1, 0, 1), (3, 6, 0, 0), (5, 4, 10, 1)])
+@pytest.mark.parametrize("alphabet,npen", [(b"ACGT", None), (b"ACGTACGTACGTN", None), (b"ACGTACGTN", 2),
+                                           (b"ACGTRY", None)])
+def test_packed_local_traceback(engine, scores, alphabet, npen):
+    # packed LOCAL+TB flags (and the int32 kernel's words for declined blocks) feed the
+    # LOCAL get_tb walk: CIGAR bytes, n_ops and the start cell it stops at
+    a, bb, o, e = scores
+    rng = np.random.default_rng(zlib.crc32(repr((scores, alphabet, npen)).encode()) & 0xFFFF)
+    qs, ts = helpers.random_pairs(rng, 900, 1, 200, 1, 250, alphabet=alphabet, related=0.6)
+    kw = dict(algo=G.LOCAL, start_pos=G.WITH_TB, match=a, mismatch=bb, gap_open=o, gap_extend=e, n_penalty=npen)
+    assert G.describe_plan(G.make_params(**kw), 200, 250).startswith("wavefront16_local_tb") or a * 200 > 255
+    check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
+
+
+def test_packed_local_traceback_config2(engine):
+    kw = dict(algo=G.LOCAL, start_pos=G.WITH_TB)
+    check(engine, no_cigar_overflow(G.Batch.synth(2, 20000, 0x5EED0002), **kw), cigar=True, **kw)
+
+
 @pytest.mark.parametrize("kw", [dict(algo=G.LOCAL), dict(algo=G.GLOBAL, start_pos=G.WITH_TB),
                                 dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET),
                                 dict(algo=G.LOCAL, start_pos=G.WITH_TB)])
