@@ -64,7 +64,15 @@ def test_decode_cigar_merges_split_runs():
 def test_plan_selection_cpu_only():
     assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150) == "wavefront16_local_G8R19"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, match=2), 150, 150) == "wavefront_local_keys_G8R20"
-    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB), 150, 150) == "wavefront_local_tb_keys_G8R20"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB), 150, 150) == "wavefront16_local_tb_G8R20"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB, match=2), 150, 150) == \
+        "wavefront_local_tb_keys_G8R20"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_START), 150, 150) == \
+        "wavefront16_local_start_G8R19"
+    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL, start_pos=G.WITH_START), 150, 182) == \
+        "wavefront16_semi_start_G8R23"
+    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL, start_pos=G.WITH_START, tail=G.QUERY), 150, 182) == \
+        "generic_semi"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, second_best=1), 150, 150) == "generic_local"
     assert G.describe_plan(G.make_params(algo=G.KSW), 150, 150) == "generic_ksw"
     assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300) == \
