@@ -97,8 +97,9 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
     return nullptr;
 }
 
-static WfFn wf16_lookup(int algo, bool tb, int G, int R) {
-    if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : wf16_pick<WF_LOCAL>(G, R);
+static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false) {
+    if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
+                                                                     : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return wf16_pick<WF_SEMI>(G, R);
 }
@@ -121,7 +122,8 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
     const int64_t q8 = pad8(mq), t8 = pad8(mt);
     if (wf_algo == WF_LOCAL) {
         const int64_t k = std::max(b, npen);
-        if (a + k > 255 || a * std::min(mq, mt) > 255 || t8 > 256) return false;   // 16-bit key: H*256 + col
+        // 16-bit keys H*256 + col: 256 columns each, a second key set up to 512 (not with traceback)
+        if (a + k > 255 || a * std::min(mq, mt) > 255 || t8 > (p.start_pos == 2 ? 256 : 512)) return false;
         const int64_t base = 0x400 + oe + k + 16;
         *vmin = 0;
         return base + 255 + a + k + 64 <= 0x7BFF;
@@ -200,11 +202,12 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             pl.lds16_stride = words * 8;                               // uint2 per position
             pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
             if (pl.G16 == 0 || pl.lds16_bytes > 160 * 1024) pl.packed16 = false;
+            pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
                        : wf_algo == WF_GLOBAL ? "global" : (p.start_pos == 1 ? "semi_start" : "semi");
         if (pl.packed16)
-            pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + "_G" + std::to_string(pl.G16) + "R" +
+            pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + (pl.key2 ? "_k2" : "") + "_G" + std::to_string(pl.G16) + "R" +
                       std::to_string(pl.R16);
         else
             pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
@@ -260,7 +263,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             HIPCHK(ws.aux.reserve((size_t)n * 4));
             P16.tbfix = ws.aux.as<int32_t>();
         }
-        WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16);
+        WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2);
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -42,6 +42,7 @@ struct Plan {
     int wf_algo = 0;        // WfAlgo
     bool keys = false, tb = false;
     bool packed16 = false;  // two pairs per lane in 16-bit halves (wavefront16.hpp), int32 fallback
+    bool key2 = false;      // packed LOCAL over 257..512 target columns (second key set)
     int G16 = 0, R16 = 0;   // packed kernel shape
     uint32_t lds16_stride = 0;
     size_t lds16_bytes = 0;

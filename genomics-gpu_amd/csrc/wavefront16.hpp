@@ -46,6 +46,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "wavefront.hpp"
 
 namespace gx {
@@ -79,6 +81,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #endif
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
+#endif
+#ifndef GX_WF16_K2_WAVES
+#define GX_WF16_K2_WAVES 2    // LOCAL over 257..512 target columns (a 3-wave build spills)
 #endif
 #ifndef GX_WF16_LTB_WAVES
 #define GX_WF16_LTB_WAVES 2   // LOCAL + traceback kernel
@@ -125,14 +130,23 @@ __device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
 // ---------------------------------------------------------------------------
 // LOCAL step: registers = query rows, one target column per step.
 // ---------------------------------------------------------------------------
-template <int R>
+// Per-row keys H*256 + (255 - column) in 16 bits cover 256 columns.  Targets up
+// to 512 columns (KM != 0) keep a second key per row for columns 256..511:
+// KM = 1 while lanes straddle column 256 (each lane feeds the key of its own
+// column's half, the other gets a 0 candidate), KM = 2 once every lane is past it.
+template <int R, int KM = 0>
 __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const uint32_t diag_top,
                                            const uint32_t f_top, const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                            uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
-                                           uint32_t &f_out, const uint32_t KK, const uint32_t OEK, const uint32_t EXT,
-                                           const uint32_t BB, const uint32_t KMUL, const uint32_t bshift) {
+                                           uint32_t (&key2)[R], uint32_t &f_out, const uint32_t KK,
+                                           const uint32_t OEK, const uint32_t EXT, const uint32_t BB,
+                                           const uint32_t KMUL, const uint32_t bshift) {
+    const bool hi = KM != 0 && c >= 256;
     const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
-    const uint32_t invc = ((col - bshift) & 0xFFFFu) * 0x10001u;   // key = H*256 + col (mod 2^16)
+    const uint32_t col2 = (c >= 256 && c < 512) ? (uint32_t)(511 - c) : 0u;
+    const uint32_t kmA = hi ? 0u : KMUL, kmB = hi ? KMUL : 0u;
+    const uint32_t invc = hi ? 0u : ((col - bshift) & 0xFFFFu) * 0x10001u;   // key = H*256 + col (mod 2^16)
+    const uint32_t invc2 = hi ? ((col2 - bshift) & 0xFFFFu) * 0x10001u : 0u;
     uint32_t diag = diag_top, f = f_top;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -143,7 +157,8 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
         Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), BB);
         f = pk_max3(toe, pk_subnb(f, EXT), BB);
-        key[k] = pk_max_u16(key[k], pk_mad_u16(H, KMUL, invc));
+        if (KM != 2) key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmA, invc));
+        if (KM != 0) key2[k] = pk_max_u16(key2[k], pk_mad_u16(H, kmB, invc2));
         diag = Hin[k];
         Hout[k] = H;
     }
@@ -303,14 +318,17 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 // ---------------------------------------------------------------------------
 constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
 constexpr int WF16_LOCAL_TB = 4;      // LOCAL with traceback words (wavefront16 only)
+constexpr int WF16_LOCAL_K2 = 5;      // LOCAL, padded targets of 257..512 columns (two keys per row)
 
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
-                                   : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
+                                   : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
+                                   : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
-    constexpr int ALGO = GTB ? WF_GLOBAL : LTB ? WF_LOCAL : ALGO_;
+    constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
+    constexpr int ALGO = GTB ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -416,9 +434,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
         const uint32_t KMUL = A.one << 8;
         const uint32_t bshift = ((uint32_t)P.base << 8) & 0xFFFFu;
-        uint32_t HA[R], HB[R], Ek[R], key[R];
+        uint32_t HA[R], HB[R], Ek[R], key[R], key2[K2 ? R : 1];
 #pragma unroll
         for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
+#pragma unroll
+        for (int k = 0; k < (K2 ? R : 1); ++k) key2[k] = 0;
         uint32_t recvH = BB, prevRecvH = BB, recvF = BB, f = BB;
         uint2 tnext = tcol[c + G];
         if constexpr (LTB) {
@@ -461,21 +481,35 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 }
             }
         } else {
-            for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-                uint2 T = tnext;
-                tnext = tcol[c + 1 + G];
-                step_local<R>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, f, KK, OEK, EXT, BB,
-                              KMUL, bshift);
-                prevRecvH = recvH;
-                recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
-                recvF = (uint32_t)shr_lane((int32_t)f);
-                T = tnext;
-                tnext = tcol[c + 2 + G];
-                step_local<R>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, f, KK, OEK, EXT,
-                              BB, KMUL, bshift);
-                prevRecvH = recvH;
-                recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
-                recvF = (uint32_t)shr_lane((int32_t)f);
+            uint32_t s = 0;
+            // two steps (ping-pong HA/HB) per iteration, up to step `end`
+            auto sweep = [&](auto kmc, const uint32_t end) {
+                constexpr int KM = decltype(kmc)::value;
+                auto &k2 = *reinterpret_cast<uint32_t(*)[R]>(K2 ? key2 : key);   // unused unless K2
+                for (; s < end; s += 2, c += 2) {
+                    uint2 T = tnext;
+                    tnext = tcol[c + 1 + G];
+                    step_local<R, KM>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, k2, f, KK,
+                                      OEK, EXT, BB, KMUL, bshift);
+                    prevRecvH = recvH;
+                    recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
+                    recvF = (uint32_t)shr_lane((int32_t)f);
+                    T = tnext;
+                    tnext = tcol[c + 2 + G];
+                    step_local<R, KM>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, k2, f,
+                                      KK, OEK, EXT, BB, KMUL, bshift);
+                    prevRecvH = recvH;
+                    recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
+                    recvF = (uint32_t)shr_lane((int32_t)f);
+                }
+            };
+            if constexpr (K2) {
+                // lane lg reaches column 256 at step 256 + lg
+                sweep(std::integral_constant<int, 0>{}, min(nsteps, 256u));
+                sweep(std::integral_constant<int, 1>{}, min(nsteps, 256u + G));
+                sweep(std::integral_constant<int, 2>{}, nsteps);
+            } else {
+                sweep(std::integral_constant<int, 0>{}, nsteps);
             }
         }
         // ---- strip-major first maximum per pair (Q1) ----
@@ -486,9 +520,12 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             for (int k = 0; k < R; ++k) {
                 const uint32_t r = r0 + k;
                 const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
-                const uint32_t H = kk >> 8;
+                uint32_t H = kk >> 8, col = 255u - (kk & 0xFFu);
+                if constexpr (K2) {   // columns 256..511: later, so they win only when strictly higher
+                    const uint32_t k2v = (key2[k] >> (16 * h)) & 0xFFFFu;
+                    if ((k2v >> 8) > H) { H = k2v >> 8; col = 511u - (k2v & 0xFFu); }
+                }
                 if (r < xpad[h] && H > 0) {
-                    const uint32_t col = 255u - (kk & 0xFFu);
                     const uint32_t ord = (((col >> 3) * xpad[h] + r) << 3) + (col & 7);
                     const uint64_t cand = ((uint64_t)H << 32) | (0xFFFFFFFFu - ord);
                     best = cand > best ? cand : best;
