@@ -291,6 +291,7 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         gx::BatchShape shape;
         shape.max_q = mq;
         shape.max_t = mt;
+        shape.sort = gx::uneven_lengths(*params, hb->q_lens + i0, hb->t_lens + i0, m);
         if ((rc = gx::align_device(s.ws, *params, db, dout, s.st, shape))) {
             for (HostSlot &x : eng->slot) (void)hipStreamSynchronize(x.st);
             return rc;
@@ -357,6 +358,7 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     gx::BatchShape shape;
     shape.max_q = db.max_q_len;
     shape.max_t = db.max_t_len;
+    shape.sort = gx::uneven_lengths(*params, hb->q_lens, hb->t_lens, n);
     rc = gx::align_device(eng->ws, *params, db, dout, st, shape);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
 #define BACK(h, d, cnt)                                                                             \

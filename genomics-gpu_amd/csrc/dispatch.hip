@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -35,7 +36,7 @@ void DevBuf::release() {
 }
 void Workspace::release_all() {
     for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
-                      &rev_t, &rev_meta}) b->release();
+                      &rev_t, &rev_meta, &sort_meta}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -342,6 +343,15 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     return GASALX_OK;
 }
 
+// GASALX_SORT=0/1 overrides the caller's BatchShape::sort (A/B and probes)
+static bool sort_wanted(const BatchShape &s) {
+    static const int force = [] {
+        const char *e = std::getenv("GASALX_SORT");
+        return e ? std::atoi(e) : -1;
+    }();
+    return force < 0 ? s.sort : force != 0;
+}
+
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
                  hipStream_t st, const BatchShape &shape, uint64_t cigar_cap) {
     if (b.n_alns == 0 || b.q_bytes == 0 || b.t_bytes == 0) { set_error("empty batch"); return GASALX_EINVAL; }
@@ -410,6 +420,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         }
     }
 
+    const uint32_t *slot_of = nullptr;   // pair -> slot when the wavefront launch ran sorted
     if (pl.kind == PLAN_WAVEFRONT) {
         WfArgs A;
         std::memset(&A, 0, sizeof(A));
@@ -422,6 +433,26 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         A.tb_pair_words = tb_words;
         A.n = n;
         A.packed = packed;
+        // uneven lengths: a wave's step count is set by its longest step-axis
+        // sequence (target; query for the transposed SEMI kernel), so run the
+        // slots in length order (counting sort, longest first)
+        if (sort_wanted(shape) && n >= 4096) {
+            const uint32_t s8w = pad8(pl.wf_algo == WF_SEMI ? shape.max_q : shape.max_t) / 8;
+            const uint32_t *slen = pl.wf_algo == WF_SEMI ? b.q_lens : b.t_lens;
+            const size_t sh = (size_t)(s8w + 1) * 4;
+            if (2 * sh <= 64 * 1024) {
+                HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + (size_t)(s8w + 1) * 8 + 64));
+                uint32_t *perm = ws.sort_meta.as<uint32_t>(), *inv = perm + n, *hist = inv + n, *cursor = hist + s8w + 1;
+                HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+                rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
+                rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
+                rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, cursor,
+                                                                          perm, inv);
+                HIPCHK(hipGetLastError());
+                A.perm = perm;
+                slot_of = inv;
+            }
+        }
         int rc = launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start) {
@@ -493,6 +524,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.pk_flags = nullptr;
         T.pk_ppb = 1; T.pk_R = 1; T.pk_rmagic = 0;
         T.pk_fix = nullptr;
+        T.slot_of = slot_of;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
         T.qseq = qsrc; T.tseq = tsrc; T.toff = b.t_offsets; T.seq_packed = packed;
         if (pl.kind == PLAN_WAVEFRONT && pl.packed16 && !pl.need_pack) {

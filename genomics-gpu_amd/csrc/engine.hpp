@@ -31,7 +31,8 @@ struct Workspace {
     DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
     DevBuf misc;                    // packed kernels: per-block "aligned here" flags
     DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
-    DevBuf rev_q, rev_t, rev_meta;  // LOCAL WITH_START: reversed slots, their offsets/lengths, reverse results
+    DevBuf rev_q, rev_t, rev_meta;  // WITH_START: reversed slots, their offsets/lengths, reverse results
+    DevBuf sort_meta;               // length sort of the forward pass: perm, inverse, histogram
     void release_all();
 };
 
@@ -57,9 +58,25 @@ struct Plan {
 // Host-visible summary of a batch needed for planning.
 struct BatchShape {
     uint32_t max_q = 0, max_t = 0;
+    bool sort = false;   // lengths are uneven: run the wavefront kernels over pairs sorted by step-axis length
 };
 
 Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
+
+// Host-side check for BatchShape::sort: the padded lengths of the step axis
+// (targets; queries for SEMI-GLOBAL, whose kernel runs transposed) spread over
+// at least two 8-base words.
+inline bool uneven_lengths(const gasalx_params &p, const uint32_t *q_lens, const uint32_t *t_lens, uint32_t n) {
+    const uint32_t *l = p.algo == 2 ? q_lens : t_lens;
+    if (!l || n == 0) return false;
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t w = (l[i] + 7) >> 3;
+        lo = w < lo ? w : lo;
+        hi = w > hi ? w : hi;
+    }
+    return hi >= lo + 2;
+}
 
 // Launch the full path for a device-resident batch on `stream`.
 // Returns GASALX_OK or an error code; sets the thread's last error message.

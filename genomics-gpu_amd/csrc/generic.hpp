@@ -424,6 +424,7 @@ struct TbArgs {
     const uint8_t *pk_flags;
     uint32_t pk_ppb, pk_R, pk_rmagic;   // pk_rmagic = ceil(2^32 / pk_R)
     const int32_t *pk_fix;              // H' at the start cell (row ql, column tl) when both are pads
+    const uint32_t *slot_of;            // pair -> slot of the DP launch when it ran sorted, or NULL
     int32_t sc_nn;                      // substitution score N vs N (GLOBAL rule)
     // sequences (as the wavefront kernels read them) for the flags' s < 0 bit
     const uint8_t *qseq, *tseq;
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int i, j, total = 0, curr = 0;
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
     else { i = (int)tl; j = (int)ql; }
-    const bool pk = A.pk_flags && A.pk_flags[tid / A.pk_ppb];
+    const bool pk = A.pk_flags && A.pk_flags[(A.slot_of ? A.slot_of[tid] : tid) / A.pk_ppb];
     const uint16_t *tb16 = reinterpret_cast<const uint16_t *>(tb);
     // packed kernel: the start cell (ql, tl), both pads, was scored with the pad
     // row's -K instead of N==N.  Its E and F are exact, so with H' the value it

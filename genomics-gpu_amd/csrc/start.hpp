@@ -60,7 +60,7 @@
 
 namespace gx {
 
-enum RevMode { REV_LOCAL = 0, REV_SEMI = 1 };
+enum RevMode { REV_LOCAL = 0, REV_SEMI = 1, REV_PLAIN = 2 };   // PLAIN: sort by the lengths given
 
 struct RevArgs {
     const uint8_t *q, *t;               // input batch (unpacked bytes or packed words)
@@ -90,6 +90,7 @@ __device__ __forceinline__ int32_t semi_gend_reg(uint32_t tl, int32_t tend) {
 
 // reversed target length of pair k
 __device__ __forceinline__ uint32_t rev_tlen(int32_t mode, const uint32_t *tlen, const int32_t *tend, uint32_t k) {
+    if (mode == REV_PLAIN) return tlen[k];
     if (mode == REV_LOCAL) return 8 * start_regs(tlen[k], tend[k]);
     const int32_t L = (int32_t)tlen[k] - 8 * semi_gend_reg(tlen[k], tend[k]);
     return (uint32_t)max(L, 0);
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256) void rev_scan_kernel(const uint32_t *hist, uin
 
 __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                           uint32_t n, uint32_t t8w, uint32_t *cursor,
-                                                          uint32_t *perm) {
+                                                          uint32_t *perm, uint32_t *inv = nullptr) {
     extern __shared__ uint32_t cnt[];   // [t8w+1] counts, then [t8w+1] bases
     uint32_t *base = cnt + t8w + 1;
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
@@ -177,7 +178,10 @@ __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const ui
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
         if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
     __syncthreads();
-    if (k < n) perm[base[b] + local] = k;
+    if (k < n) {
+        perm[base[b] + local] = k;
+        if (inv) inv[k] = base[b] + local;
+    }
 }
 
 // one thread per (slot, 8-base word of the two reversed sequences of the slot's pair)

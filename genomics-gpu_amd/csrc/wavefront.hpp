@@ -47,6 +47,7 @@ struct WfArgs {
     const uint8_t *skip;       // int32 kernel: pairs whose packed block already aligned them
     uint32_t skip_ppb;         // pairs per packed block
     int32_t *tbfix;            // wavefront16 GLOBAL+TB: H at the traceback start cell (ql, tl), see tb_kernel
+    const uint32_t *perm;      // slot -> pair (pairs sorted by step-axis length, dispatch.hip), or NULL
     const int32_t *stop;       // SEMI TAIL=TARGET reverse pass (start.hpp): per pair, the forward score; the
                                // last-row maximum is then taken inside the first 8-column strip holding a
                                // value >= it (the reference's early exit), else over the whole row
@@ -342,9 +343,10 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     const uint32_t lg = lane & (G - 1);
     const uint32_t slot = lane / G;
     const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * P;
-    const uint32_t pair = pair0 + slot;
-    // pairs the packed kernel already aligned are skipped (dispatch.hip)
-    const bool valid = pair < A.n && !(A.skip && A.skip[pair / A.skip_ppb]);
+    const uint32_t idx = pair0 + slot;   // slot; the pair is perm[slot] when sorted
+    // pairs the packed kernel already aligned are skipped (dispatch.hip); its flags are per block of slots
+    const bool valid = idx < A.n && !(A.skip && A.skip[idx / A.skip_ppb]);
+    const uint32_t pair = (valid && A.perm) ? A.perm[idx] : idx;
     if (A.skip && !__syncthreads_or(valid)) return;      // block-uniform early exit
 
     uint32_t ql = 0, tl = 0, qo = 0, to = 0;

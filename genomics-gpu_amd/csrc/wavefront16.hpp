@@ -339,8 +339,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     const uint8_t *X = TR ? A.t : A.q, *Y = TR ? A.q : A.t;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        pr[h] = pair0 + 2 * slot + h;
-        valid[h] = pr[h] < A.n;
+        const uint32_t idx = pair0 + 2 * slot + h;   // slot; the pair is perm[slot] when sorted
+        valid[h] = idx < A.n;
+        pr[h] = (valid[h] && A.perm) ? A.perm[idx] : idx;
         const uint32_t ql = valid[h] ? A.qlen[pr[h]] : 0, tl = valid[h] ? A.tlen[pr[h]] : 0;
         const uint32_t qo = valid[h] ? A.qoff[pr[h]] : 0, to = valid[h] ? A.toff[pr[h]] : 0;
         xl[h] = TR ? tl : ql; yl[h] = TR ? ql : tl;

@@ -170,6 +170,40 @@ def test_local_with_start_packed_and_ops(engine):
     check(engine, b, q_ops=qo, t_ops=to, algo=G.LOCAL, start_pos=G.WITH_START)
 
 
+@pytest.mark.parametrize("alphabet,scores", [(b"ACGT", (1, 4, 6, 1)), (b"ACGTN", (2, 3, 5, 2)),
+                                             (b"ACGTRY", (1, 4, 6, 1))])
+def test_local_long_targets_two_keys(engine, alphabet, scores):
+    # packed LOCAL over 257..512 target columns keeps a second key set per row
+    a, bb, o, e = scores
+    kw = dict(algo=G.LOCAL, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+    assert G.describe_plan(G.make_params(**kw), 120, 512) == "wavefront16_local_k2_G8R16"
+    rng = np.random.default_rng(zlib.crc32(repr((alphabet, scores)).encode()) & 0xFFFF)
+    qs, ts = helpers.random_pairs(rng, 1500, 1, 120, 200, 512, alphabet=alphabet, related=0.5)
+    # ties across the 256-column boundary: a repeated block on both sides of it
+    rep = helpers.random_seq(rng, 40)
+    qs += [rep] * 20
+    ts += [helpers.random_seq(rng, 230 + i) + rep + helpers.random_seq(rng, 10) + rep for i in range(20)]
+    check(engine, G.Batch.from_pairs(qs, ts), **kw)
+    check(engine, G.Batch.from_pairs(qs[:600], ts[:600]), start_pos=G.WITH_START, **kw)
+
+
+@pytest.mark.parametrize("kw", [dict(algo=G.LOCAL), dict(algo=G.LOCAL, start_pos=G.WITH_START),
+                                dict(algo=G.LOCAL, start_pos=G.WITH_TB), dict(algo=G.GLOBAL),
+                                dict(algo=G.GLOBAL, start_pos=G.WITH_TB),
+                                dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET),
+                                dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
+                                     max_query_len=512),
+                                dict(algo=G.SEMI_GLOBAL, head=G.BOTH, tail=G.BOTH)])
+def test_length_sorted_launch(engine, kw):
+    # >= 4096 pairs of uneven lengths through the host entry: the wavefront kernels
+    # run over pairs sorted by step-axis length (dispatch.hip), results in pair order
+    rng = np.random.default_rng(zlib.crc32(repr(kw).encode()) & 0xFFFF)
+    qs, ts = helpers.random_pairs(rng, 5000, 1, 200, 1, 300, alphabet=b"ACGTACGTACGTN", related=0.6)
+    b = G.Batch.from_pairs(qs, ts)
+    tb = kw.get("start_pos") == G.WITH_TB
+    check(engine, no_cigar_overflow(b, **kw) if tb else b, cigar=tb, **kw)
+
+
 def test_local_second_best(engine):
     check(engine, rand_batch(22, 600, 30, 150, 30, 200), algo=G.LOCAL, second_best=1)
 

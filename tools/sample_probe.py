@@ -60,4 +60,5 @@ for name in modes:
                       "pairs": b.n, "mean_q": round(float(b.q_lens.mean()), 1),
                       "mean_t": round(float(b.t_lens.mean()), 1), "ms": round(ms, 3),
                       "gcups": round(cells / ms / 1e6, 1),
-                      "lib": os.path.basename(os.environ.get("GASALX_LIB", "libgasal.so"))}), flush=True)
+                      "lib": os.path.basename(os.environ.get("GASALX_LIB", "libgasal.so")),
+                      "sort": os.environ.get("GASALX_SORT", "auto")}), flush=True)
