@@ -45,8 +45,10 @@ struct Shape { int G, R; };
 static const Shape kShapes[] = {{8, 8}, {8, 12}, {8, 16}, {8, 20}, {16, 16}, {16, 20}, {32, 20}, {64, 20}};
 // packed kernels (register axis = query for LOCAL/GLOBAL, target for SEMI):
 // R = 19 fits 150 bp (152 padded) and R = 23 fits 182 bp (184 padded) exactly
-static const Shape kShapes16[] = {{8, 8},   {8, 12},  {8, 16},  {8, 19},  {8, 20},
-                                  {8, 23},  {16, 16}, {16, 20}, {32, 20}, {64, 20}};
+// G = 16/32/64 shapes with few rows per lane serve small batches (make_plan)
+static const Shape kShapes16[] = {{8, 8},   {8, 12},  {8, 16},  {8, 19},  {8, 20},  {8, 23},  {16, 10}, {16, 12},
+                                  {16, 16}, {16, 20}, {32, 5},  {32, 6},  {32, 9},  {32, 20}, {64, 3},  {64, 5},
+                                  {64, 20}};
 
 using WfFn = void (*)(WfArgs);
 
@@ -77,7 +79,8 @@ template <int ALGO>
 static WfFn wf16_pick(int G, int R) {
 #define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<ALGO, g, r>;
     GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 20) GX_CASE(8, 23)
-    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+    GX_CASE(16, 10) GX_CASE(16, 12) GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 5) GX_CASE(32, 6) GX_CASE(32, 9)
+    GX_CASE(32, 20) GX_CASE(64, 3) GX_CASE(64, 5) GX_CASE(64, 20)
 #undef GX_CASE
     return nullptr;
 }
@@ -110,7 +113,8 @@ static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
 // The packed kernels (wavefront16.hpp) are exact when every stored value stays
 // inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
 // fit bytes.  Mirrors pk16_params; returns false to keep the int32 kernel.
-static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin) {
+static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32_t mt, int32_t *vmin,
+                        int64_t span = 0) {
     if (p.second_best || (p.start_pos == 1 && wf_algo == WF_GLOBAL)) return false;
     if (p.start_pos == 2 && wf_algo == WF_SEMI) return false;     // no traceback for SEMI (reference)
     // GLOBAL+TB reads the first pad query row, scored -K = -max(b, npen) there:
@@ -139,11 +143,17 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
         k = 2 * drift;                                         // table offset K = 2D (pk16_params)
     }
     if (a + k > 255) return false;
-    const int64_t v = 4 * oe + k + e * (q8 + t8) + 2 * drift + 64;   // below every reachable value
+    // span: largest row + column of any cell the launch computes.  Both halves of
+    // a register hold the same cell of two pairs of different lengths, so one
+    // pair's pad cells share 32-bit adds with the other's real cells: every
+    // computed cell (register rows up to G*R, steps past the longest sequence)
+    // must stay inside the window or a borrow corrupts the neighbour (SEMI keeps
+    // no floor on E/F; values fall by at most e per row or column along a gap).
+    // make_plan checks again with the chosen shape's span.
+    if (!span) span = q8 + t8 + 2 * 64 + 8;
+    const int64_t v = 4 * oe + k + e * span + 2 * drift + 64;   // below every reachable value
     const int64_t neg = 0x400 + 2 * e + 16;
-    // + the drift over the anti-diagonals a lane sweeps (incl. up to 64+4 steps of
-    //   garbage before the reset / after the last column)
-    top = neg + v + a * std::min(q8, t8) + a + k + oe + 64 + drift * (q8 + t8 + 2 * 64 + 8);
+    top = neg + v + a * std::min(q8, t8) + a + k + oe + 64 + drift * span;
     if (top > 0x7BFF) return false;
     *vmin = (int32_t)v;
     return true;
@@ -197,12 +207,31 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         if (pl.packed16) {
             const uint32_t x8 = (wf_algo == WF_SEMI) ? t8 : q8, y8 = (wf_algo == WF_SEMI) ? q8 : t8;
             pl.G16 = 0;
+            // small batches: enough lanes per pair that the launch still holds about two
+            // waves per SIMD (128/G pairs per wave, 1024 SIMDs); traceback keeps G = 8 up
+            static const int gforce = [] {   // GASALX_GMIN: fixed minimum G (A/B, debugging)
+                const char *v = std::getenv("GASALX_GMIN");
+                return v ? std::atoi(v) : 0;
+            }();
+            uint32_t gmin = 8;
+            // (not SEMI: its WITH_START reverse pass disagreed with the oracle on 3 of
+            // 1,000 pairs at G = 64, cause not yet found; GASALX_GMIN still forces it)
+            if (s.n && !pl.tb && wf_algo != WF_SEMI)
+                while (gmin < 64 && (uint64_t)s.n * gmin < 2048ull * 128) gmin *= 2;
+            if (gforce > 0) gmin = (uint32_t)gforce;
             for (const Shape &sh : kShapes16)
-                if ((uint32_t)(sh.G * sh.R) >= x8 && !(pl.tb && sh.R % 4)) { pl.G16 = sh.G; pl.R16 = sh.R; break; }
+                if ((uint32_t)sh.G >= gmin && (uint32_t)(sh.G * sh.R) >= x8 &&
+                    !(pl.tb && (sh.R % 4 || (sh.G > 8 && sh.R < 16)))) {
+                    pl.G16 = sh.G; pl.R16 = sh.R;
+                    break;
+                }
             const uint32_t words = (y8 + 2 * pl.G16 + 4 + 3) & ~3u;   // odd-step tail + prefetch
             pl.lds16_stride = words * 8;                               // uint2 per position
             pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
             if (pl.G16 == 0 || pl.lds16_bytes > 160 * 1024) pl.packed16 = false;
+            if (pl.packed16 && wf_algo != WF_LOCAL)   // the value window over the chosen shape's cells
+                pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin,
+                                          (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8);
             pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
@@ -324,7 +353,7 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     HIPCHK(hipGetLastError());
     gasalx_params pr = p;
     pr.start_pos = 0;
-    BatchShape rs; rs.max_q = q8; rs.max_t = t8;
+    BatchShape rs; rs.max_q = q8; rs.max_t = t8; rs.n = n;
     const Plan pl = make_plan(pr, rs, false);
     if (pl.kind != PLAN_WAVEFRONT) { set_error("reverse pass has no wavefront plan"); return GASALX_EUNSUPPORTED; }
     WfArgs A;
@@ -360,7 +389,9 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     if (p.algo == 6 && !b.seed_scores) { set_error("KSW needs seed_scores"); return GASALX_EINVAL; }
     if (shape.max_q == 0 || shape.max_t == 0) { set_error("zero-length sequence"); return GASALX_ERANGE; }
     const bool has_ops = b.q_ops && b.t_ops;
-    Plan pl = make_plan(p, shape, has_ops);
+    BatchShape sized = shape;
+    sized.n = b.n_alns;
+    Plan pl = make_plan(p, sized, has_ops);
     const uint32_t n = b.n_alns;
     const bool tb = p.start_pos == 2;
 

@@ -59,6 +59,7 @@ struct Plan {
 struct BatchShape {
     uint32_t max_q = 0, max_t = 0;
     bool sort = false;   // lengths are uneven: run the wavefront kernels over pairs sorted by step-axis length
+    uint32_t n = 0;      // pairs in the launch (0 = unknown: shapes for large batches)
 };
 
 Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
