@@ -29,12 +29,13 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_sw_local 600 python bench.py
 step bench_sw_local_start 600 python bench.py --workload sw_local_start --steps 10 --cpu-seconds 8
 step bench_nw_tb 600 python bench.py --workload nw_tb --no-cpu --steps 10
+step bench_sw_local_tb 600 python bench.py --workload sw_local_tb --no-cpu --steps 10
 step bench_semi 600 python bench.py --workload semi --no-cpu --steps 10
 step bench_semi_start 600 python bench.py --workload semi_start --no-cpu --steps 10
 step path_probe 600 python tools/path_probe.py 200000
 step bench_pairhmm 600 python bench.py --workload pairhmm --steps 10 --cpu-seconds 8
 cd /tmp && export TMPDIR=/tmp
-for w in ${PROF_WORKLOADS:-sw_local sw_local_start nw_tb semi semi_start pairhmm}; do
+for w in ${PROF_WORKLOADS:-sw_local sw_local_start sw_local_tb nw_tb semi semi_start pairhmm}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/prof_$w" -o run -- python3 "$ROOT/bench.py" --workload $w --steps 10 --warmup 2 --no-cpu --no-e2e > "$ROOT/$O/bench_prof_$w.out" 2> "$ROOT/$O/bench_prof_$w.err"
   rc=$?; echo "[rocprof $w] rc=$rc"
   if fatal $rc; then exit $rc; fi
