@@ -287,7 +287,9 @@ def main():
                        "parallelism": f"dp{world} (pairs sharded)" + (", all-gather of scores" if gathered else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "bytes_per_pair": bytes_per_pair, "kernel_ms": round(kern_ms, 4)},
+                         "bytes_per_pair": bytes_per_pair, "kernel_ms": round(kern_ms, 4),
+                         "timed": "HIP events around the whole step on its stream (every kernel of the step; "
+                                  "WITH_START/WITH_TB steps launch more than the dominant kernel)"},
             "valu_roofline": valu_roof,
             "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),

@@ -2,8 +2,7 @@
 """Summarise a scripts/pmc_session.sh run into profiles/pmc_<workload>.json.
 
 usage: pmc_summary.py RUN_DIR WORKLOAD PAIRS_PER_LAUNCH
-For the dominant kernel of the bench step (the longest dispatch of the last
-bench step), records every counter of every pass and the derived:
+For the dominant kernel of the bench step (its longest dispatch), records every counter of every pass and the derived:
   hbm_bytes_per_launch   = 2 x FETCH_SIZE + WRITE_SIZE (KB -> bytes; gfx950
                            FETCH_SIZE tallies 128-B requests at 64 B, see
                            MI355X_MICROARCH.md, HBM section)
@@ -20,20 +19,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main(run_dir, workload, pairs):
-    per = collections.defaultdict(dict)   # kernel -> counter -> value (last dispatch of that kernel)
+    per = collections.defaultdict(dict)   # kernel -> counter -> value (its longest dispatch in the pass)
     dur = {}
     for path in sorted(glob.glob(os.path.join(run_dir, "p*", "run_counter_collection.csv"))):
         rows = list(csv.DictReader(open(path)))
         agg = collections.defaultdict(float)
-        last = {}
+        pdur = {}
         for r in rows:
             k = r["Kernel_Name"]
             d = int(r["Dispatch_Id"])
             agg[(k, d, r["Counter_Name"])] += float(r["Counter_Value"])
-            last[k] = max(last.get(k, -1), d)
-            dur[(k, d)] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            pdur[(k, d)] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        # a kernel launched twice per step (WITH_START: forward and reverse pass)
+        # is summarised by its longest dispatch, the forward pass
+        longest = {}
+        for (k, d), t in pdur.items():
+            if t > pdur.get((k, longest.get(k, -1)), -1):
+                longest[k] = d
+        dur.update(pdur)
         for (k, d, c), v in agg.items():
-            if d == last[k]:
+            if d == longest[k]:
                 per[k][c] = v
     # dominant kernel: longest last dispatch
     best = max(per, key=lambda k: max(v for (kk, _), v in dur.items() if kk == k))
@@ -44,7 +49,7 @@ def main(run_dir, workload, pairs):
     if "SQ_INSTS_VALU" in c:
         out["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
     out["note"] = ("separate rocprofv3 --pmc passes (scripts/pmc_session.sh); FETCH_SIZE x2 per the gfx950 "
-                   "correction; counters of the last dispatch of the dominant kernel")
+                   "correction; counters of the longest dispatch of the dominant kernel")
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
     print(path, {k: out[k] for k in out if k not in ("counters", "note")})
