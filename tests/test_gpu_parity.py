@@ -275,6 +275,17 @@ def test_semiglobal_with_start_wavefront(engine, head, alphabet, scores):
     check(engine, b, **kw)
 
 
+@pytest.mark.parametrize("head", [G.NONE, G.TARGET])
+def test_semiglobal_long_targets_wide_groups(engine, head):
+    # targets past 320 columns take the G = 32 / 64 packed shapes (R = 20)
+    kw = dict(algo=G.SEMI_GLOBAL, head=head, tail=G.TARGET, match=1, mismatch=4, gap_open=6, gap_extend=1,
+              max_query_len=512)
+    assert G.describe_plan(G.make_params(**kw), 200, 600) == "wavefront16_semi_G32R20"
+    b = rand_batch(0x5E31 + head, 600, 1, 200, 330, 600, related=0.6)
+    check(engine, b, **kw)
+    check(engine, b, start_pos=G.WITH_START, **kw)
+
+
 def test_semiglobal_with_start_reads_in_windows(engine):
     kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START, max_query_len=192)
     check(engine, G.Batch.synth(4, 20000, 0x5EED0004), **kw)
