@@ -275,6 +275,20 @@ def test_semiglobal_with_start_wavefront(engine, head, alphabet, scores):
     check(engine, b, **kw)
 
 
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2)])
+@pytest.mark.parametrize("head", [G.NONE, G.TARGET])
+def test_semiglobal_targets_to_192(engine, head, scores):
+    # padded targets of 185..192 take a G = 16 shape; SEMI must keep R >= 16 there
+    # (the few-row wide shapes disagreed with the oracle, DESIGN.md "Small batches")
+    a, bb, o, e = scores
+    kw = dict(algo=G.SEMI_GLOBAL, head=head, tail=G.TARGET, match=a, mismatch=bb, gap_open=o, gap_extend=e,
+              max_query_len=512)
+    assert G.describe_plan(G.make_params(**kw), 200, 190) == "wavefront16_semi_G16R16"
+    b = rand_batch(0x5E32 + 7 * head + a, 1000, 1, 200, 1, 190, related=0.6)
+    check(engine, b, **kw)
+    check(engine, b, start_pos=G.WITH_START, **kw)
+
+
 @pytest.mark.parametrize("head", [G.NONE, G.TARGET])
 def test_semiglobal_long_targets_wide_groups(engine, head):
     # targets past 320 columns take the G = 32 / 64 packed shapes (R = 20)
