@@ -163,6 +163,35 @@ SENTINEL = -(2 ** 31) + 7
 OUT_FIELDS = ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")
 
 
+class PinnedHost:
+    """Page-locked host bytes from the engine's own HIP runtime (hipHostMalloc in the
+    libamdhip64 libgasal links; torch ships a second runtime whose pinned pages this
+    one would treat as pageable).  For caller-owned result buffers such as
+    align_host(cigar_out=...), as the reference's host_res is pinned (res.cpp:8-70).
+    `array` is valid until close()."""
+
+    def __init__(self, nbytes: int):
+        lib()
+        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        self._p = ctypes.c_void_p()
+        rc = self._hip.hipHostMalloc(ctypes.byref(self._p), ctypes.c_size_t(max(int(nbytes), 1)), ctypes.c_uint(0))
+        if rc != 0 or not self._p.value:
+            raise RuntimeError(f"hipHostMalloc({nbytes}) failed: {rc}")
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(self._p.value))
+
+    def close(self):
+        if self._p is not None and self._p.value:
+            self.array = None
+            self._hip.hipHostFree(self._p)
+        self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """One device workspace + stream (gasalx_engine)."""
 
@@ -181,12 +210,21 @@ class Engine:
         except Exception:
             pass
 
-    def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None, fields=None):
-        """fields: the result arrays to request (default all; the rest are passed as NULL)."""
+    def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None, fields=None,
+                   cigar_out=None):
+        """fields: the result arrays to request (default all; the rest are passed as NULL).
+        cigar_out: optional caller-owned uint8 array of q_bytes for the CIGAR buffer (e.g. a
+        page-locked one, as the reference's own host_res, res.cpp:8-70), used as given."""
         n = batch.n
         out = {k: np.full(n, SENTINEL, np.int32) for k in (OUT_FIELDS if fields is None else fields)}
         tb = params.start_pos == WITH_TB          # CIGAR buffers only when the reference fills them
-        cigar = np.zeros(batch.q_bytes if tb else 0, np.uint8)
+        if cigar_out is not None:
+            if not (tb and isinstance(cigar_out, np.ndarray) and cigar_out.dtype == np.uint8
+                    and cigar_out.ndim == 1 and cigar_out.size >= batch.q_bytes and cigar_out.flags.c_contiguous):
+                raise ValueError("cigar_out: contiguous uint8 array of at least q_bytes, WITH_TB only")
+            cigar = cigar_out
+        else:
+            cigar = np.zeros(batch.q_bytes if tb else 0, np.uint8)
         n_ops = np.zeros(n if tb else 0, np.uint32)
         qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
         to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)

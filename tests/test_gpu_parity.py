@@ -539,3 +539,22 @@ def test_pairhmm_edge_lengths(engine):
                               dq=rng.integers(10, 60, R)))
     args = _hmm_batch(pairs)
     np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
+
+
+def test_host_pipeline_pinned_cigar(engine):
+    # a caller-owned page-locked CIGAR buffer (bench.py end_to_end "pinned_cigar") must
+    # come back byte-identical to the library-allocated one, whatever it held before
+    rng = np.random.default_rng(0x919F)
+    qs, ts = helpers.random_pairs(rng, 40000, 8, 72, 8, 80)
+    kw = dict(algo=G.LOCAL, start_pos=G.WITH_TB)
+    batch = no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw)
+    gp = G.make_params(**kw)
+    ref = engine.align_host(batch, gp)
+    host = G.PinnedHost(batch.q_bytes)
+    pinned = host.array
+    pinned[:] = 0xFF
+    got = engine.align_host(batch, gp, cigar_out=pinned)
+    assert got["cigar"] is pinned
+    for f in ("score", "q_end", "t_end", "q_start", "t_start", "n_ops", "cigar"):
+        assert np.array_equal(got[f], ref[f]), f
+    host.close()
