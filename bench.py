@@ -12,6 +12,7 @@ barrier + synchronize and the max over ranks is reported.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--workload sw_local|nw_tb|semi|pairhmm]
 """
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -171,6 +172,20 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
         dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, cigar_out=host.array))
         host.close()
         res["pinned_cigar"] = {"value": round(cells / dtp / 1e9, 2), "ms_per_batch": round(dtp * 1e3, 3)}
+    if kind != 5:
+        # sequence bytes page-locked too, as the reference's host batch pages are
+        # (host_batch.cpp:79-153 fills pinned pages), plus the CIGAR buffer for TB
+        hq, ht = G.PinnedHost(data.q_bytes), G.PinnedHost(data.t_bytes)
+        hq.array[:] = data.q_data
+        ht.array[:] = data.t_data
+        pb = dataclasses.replace(data, q_data=hq.array, t_data=ht.array)
+        hc = G.PinnedHost(data.q_bytes) if params.start_pos == G.WITH_TB else None
+        dtp, _ = timed(lambda: eng.align_host(pb, params, fields=fields, cigar_out=hc.array if hc else None))
+        res["pinned_io"] = {"value": round(cells / dtp / 1e9, 2), "ms_per_batch": round(dtp * 1e3, 3),
+                            "pinned": "q/t sequence bytes" + (" + CIGAR buffer" if hc else "")}
+        for h in (hq, ht, hc):
+            if h:
+                h.close()
     return res
 
 
