@@ -172,6 +172,8 @@ class PinnedHost:
 
     def __init__(self, nbytes: int):
         lib()
+        self._p = None
+        # the soname libgasal.so records (ldd: libamdhip64.so.7 on ROCm 7), already loaded
         self._hip = ctypes.CDLL("libamdhip64.so.7")
         self._p = ctypes.c_void_p()
         rc = self._hip.hipHostMalloc(ctypes.byref(self._p), ctypes.c_size_t(max(int(nbytes), 1)), ctypes.c_uint(0))
