@@ -558,3 +558,19 @@ def test_host_pipeline_pinned_cigar(engine):
     for f in ("score", "q_end", "t_end", "q_start", "t_start", "n_ops", "cigar"):
         assert np.array_equal(got[f], ref[f]), f
     host.close()
+
+
+@pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL])
+def test_host_pipeline_tb_slot_reuse(engine, algo):
+    # TB batches are chunked by padded cells (capi.cpp gasalx_align_host): one
+    # 448 x 448 pair among 80 K short ones gives 80 K x 448^2 / 5.5 G -> 3 chunks, so
+    # slot 0 is drained (results + CIGAR bytes back) before it takes chunk 2
+    rng = np.random.default_rng(0x91A0)
+    qs, ts = helpers.random_pairs(rng, 80000, 8, 72, 8, 80)
+    long_seq = helpers.random_seq(rng, 448, b"ACGT")
+    qs[40000], ts[40000] = long_seq, long_seq
+    kw = dict(algo=algo, start_pos=G.WITH_TB)
+    batch = no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw)
+    mq, mt = int(batch.q_lens.max()), int(batch.t_lens.max())
+    assert batch.n * mq * mt / 5.5e9 >= 2.5, (batch.n, mq, mt)
+    check(engine, batch, cigar=True, **kw)
