@@ -209,22 +209,20 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             pl.G16 = 0;
             // small batches: enough lanes per pair that the launch still holds about two
             // waves per SIMD (128/G pairs per wave, 1024 SIMDs); traceback keeps G = 8 up
-            static const int gforce = [] {   // GASALX_GMIN: fixed minimum G (A/B, debugging)
-                const char *v = std::getenv("GASALX_GMIN");
-                return v ? std::atoi(v) : 0;
-            }();
+            // GASALX_GMIN: fixed minimum G (A/B runs, parity sweeps); read per call so a
+            // test process can sweep it
+            const char *gmin_env = std::getenv("GASALX_GMIN");
+            const int gforce = gmin_env ? std::atoi(gmin_env) : 0;
             uint32_t gmin = 8;
-            // (not SEMI: its WITH_START reverse pass disagreed with the oracle on 3 of
-            // 1,000 pairs at G = 64, cause not yet found; GASALX_GMIN still forces it)
-            if (s.n && !pl.tb && wf_algo != WF_SEMI)
+            if (s.n && !pl.tb)
                 while (gmin < 64 && (uint64_t)s.n * gmin < 2048ull * 128) gmin *= 2;
             if (gforce > 0) gmin = (uint32_t)gforce;
+            // traceback kernels store flags in groups of 4 rows and keep >= 16 rows per
+            // lane (their instances, wf16_pick_tb): the other shapes are never taken,
+            // forced or not
             for (const Shape &sh : kShapes16)
                 if ((uint32_t)sh.G >= gmin && (uint32_t)(sh.G * sh.R) >= x8 &&
-                    !(pl.tb && (sh.R % 4 || (sh.G > 8 && sh.R < 16))) &&
-                    // SEMI disagrees with the oracle on a few pairs per thousand on shapes with
-                    // G > 8 and R < 16 (tools/semi_start_debug.py; cause open): not used
-                    !(wf_algo == WF_SEMI && sh.G > 8 && sh.R < 16)) {
+                    !(pl.tb && (sh.R % 4 || (sh.G > 8 && sh.R < 16)))) {
                     pl.G16 = sh.G; pl.R16 = sh.R;
                     break;
                 }

@@ -702,7 +702,14 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             for (int h = 0; h < 2; ++h)
                 if (valid[h]) thrp[h] = A.stop[pr[h]] + pb - oe;   // stored pattern of the forward score
         }
-        uint32_t recvH = HA[R - 1], prevRecvH = HA[R - 1], recvE = NN, hl = 0, el = 0;
+        // Lane lg's first real step (row 0, column r0) takes its diagonal from the
+        // upper lane's reset at row -1, i.e. H(-1, r0 - 1).  Lanes lg >= 2 receive it
+        // by the hand-off of that reset step; lane 1's upper lane (lane 0) has no
+        // reset step, so the value is seeded here.  Seeding it with the lane's own
+        // H(-1, r0 + R - 1) made cell (0, R) of lane 1 wrong with HEAD=NONE, which
+        // surfaced on few-row shapes (the diagonal entry at column R is cheap there).
+        const uint32_t hd_up = hm(head_t ? 0 : (r0 == 0 ? 0 : -(go + ge * (int32_t)r0)));
+        uint32_t recvH = hd_up, prevRecvH = hd_up, recvE = NN, hl = 0, el = 0;
         uint2 tnext = tcol[c + G];
         auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
             const uint2 T = tnext;

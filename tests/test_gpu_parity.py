@@ -278,12 +278,12 @@ def test_semiglobal_with_start_wavefront(engine, head, alphabet, scores):
 @pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2)])
 @pytest.mark.parametrize("head", [G.NONE, G.TARGET])
 def test_semiglobal_targets_to_192(engine, head, scores):
-    # padded targets of 185..192 take a G = 16 shape; SEMI must keep R >= 16 there
-    # (the few-row wide shapes disagreed with the oracle, DESIGN.md "Small batches")
+    # padded targets of 185..192 take the G = 16, R = 12 shape (the few-row wide shapes
+    # once disagreed with the oracle with HEAD=NONE, fixed: test_semiglobal_every_packed_shape)
     a, bb, o, e = scores
     kw = dict(algo=G.SEMI_GLOBAL, head=head, tail=G.TARGET, match=a, mismatch=bb, gap_open=o, gap_extend=e,
               max_query_len=512)
-    assert G.describe_plan(G.make_params(**kw), 200, 190) == "wavefront16_semi_G16R16"
+    assert G.describe_plan(G.make_params(**kw), 200, 190) == "wavefront16_semi_G16R12"
     b = rand_batch(0x5E32 + 7 * head + a, 1000, 1, 200, 1, 190, related=0.6)
     check(engine, b, **kw)
     check(engine, b, start_pos=G.WITH_START, **kw)
@@ -574,3 +574,77 @@ def test_host_pipeline_tb_slot_reuse(engine, algo):
     mq, mt = int(batch.q_lens.max()), int(batch.t_lens.max())
     assert batch.n * mq * mt / 5.5e9 >= 2.5, (batch.n, mq, mt)
     check(engine, batch, cigar=True, **kw)
+
+
+# ------------------------------------------------- every packed shape ----
+# (G, R) of kShapes16 (dispatch.hip).  GASALX_GMIN forces the minimum G; the
+# padded register-axis length G*R then selects exactly that shape.
+SHAPES16 = [(8, 8), (8, 12), (8, 16), (8, 19), (8, 20), (8, 23), (16, 10), (16, 12), (16, 16), (16, 20),
+            (32, 5), (32, 6), (32, 9), (32, 20), (64, 3), (64, 5), (64, 20)]
+SEMI_SCORES = [(1, 4, 6, 1), (2, 3, 5, 2), (3, 5, 4, 3)]   # every set keeps o+e >= b (packed SEMI)
+
+
+def _forced_g(monkeypatch, g):
+    monkeypatch.setenv("GASALX_GMIN", str(g))
+
+
+def _shape_batch(seed, n, qmax, tmax, fix_q=None, fix_t=None):
+    rng = np.random.default_rng(seed)
+    qs, ts = helpers.random_pairs(rng, n, 1, qmax, 1, tmax, related=0.6)
+    # one pair at the full register-axis length, so the padded maximum selects the shape
+    if fix_t:
+        ts[0] = (ts[0] * (fix_t // max(1, len(ts[0])) + 1))[:fix_t]
+    if fix_q:
+        qs[1] = (qs[1] * (fix_q // max(1, len(qs[1])) + 1))[:fix_q]
+    return G.Batch.from_pairs(qs, ts)
+
+
+@pytest.mark.parametrize("g,r", SHAPES16)
+def test_semiglobal_every_packed_shape(engine, monkeypatch, g, r):
+    """Packed SEMI (registers = target columns) forced onto every (G, R) shape, all
+    four HEADs x three score sets, score-only and WITH_START (TAIL=TARGET).  The few-row
+    wide shapes once disagreed with the oracle with HEAD=NONE: lane 1's diagonal into
+    (row 0, column R) was seeded with the wrong top-boundary value (wavefront16.hpp)."""
+    _forced_g(monkeypatch, g)
+    tl = g * r
+    b = _shape_batch(0x5A00 + g * 31 + r, 300, 200, tl, fix_t=tl)
+    for head in (G.NONE, G.QUERY, G.TARGET, G.BOTH):
+        for a, bb, o, e in SEMI_SCORES:
+            kw = dict(algo=G.SEMI_GLOBAL, head=head, tail=G.TARGET, match=a, mismatch=bb, gap_open=o,
+                      gap_extend=e, max_query_len=max(512, tl))
+            assert G.describe_plan(G.make_params(**kw), 200, tl) == f"wavefront16_semi_G{g}R{r}"
+            check(engine, b, **kw)
+            check(engine, b, start_pos=G.WITH_START, **kw)
+
+
+def test_semiglobal_head_none_entry_at_lane_boundary(engine, monkeypatch):
+    """Known answer for the fixed lane-1 seed: with HEAD=NONE the best alignment enters
+    row 0 diagonally from the top boundary at column R - 1, cost -(o + e*R) (Q3/Q2
+    textbook diagonal, semiglobal_kernel_template.h:123-128).  Query = target[R:R+40]."""
+    rng = np.random.default_rng(0x5A11)
+    for g, r in [(64, 3), (32, 5), (16, 10), (8, 19)]:
+        _forced_g(monkeypatch, g)
+        tl = g * r
+        t = helpers.random_seq(rng, tl)
+        q = t[r:r + 40]
+        b = G.Batch.from_pairs([q, q], [t, t])
+        kw = dict(algo=G.SEMI_GLOBAL, head=G.NONE, tail=G.TARGET, max_query_len=max(512, tl))
+        assert G.describe_plan(G.make_params(**kw), 40, tl) == f"wavefront16_semi_G{g}R{r}"
+        g_, o_ = check(engine, b, **kw)
+        # 40 matches after a top-boundary diagonal of -(6 + 1*r)
+        assert int(o_["score"][0]) == 40 - (6 + r) and int(o_["t_end"][0]) == r + 39
+
+
+@pytest.mark.parametrize("g,r", SHAPES16)
+@pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL])
+def test_local_global_every_packed_shape(engine, monkeypatch, algo, g, r):
+    """LOCAL / GLOBAL packed kernels (registers = query rows) forced onto every shape."""
+    _forced_g(monkeypatch, g)
+    ql = g * r
+    b = _shape_batch(0x5B00 + g * 31 + r + algo, 300, ql, 240, fix_q=ql)
+    # LOCAL packs only while a * min(ql, tl) <= 255 (16-bit keys): match 1
+    for a, bb, o, e in [(1, 4, 6, 1), (1, 3, 5, 2), (1, 2, 2, 1)]:
+        kw = dict(algo=algo, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+        plan = G.describe_plan(G.make_params(**kw), ql, 240)
+        assert plan == f"wavefront16_{'local' if algo == G.LOCAL else 'global'}_G{g}R{r}", plan
+        check(engine, b, **kw)
