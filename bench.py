@@ -1,71 +1,151 @@
 #!/usr/bin/env python3
-"""Benchmark of the hot path: batched affine-gap Smith-Waterman (GASAL2 LOCAL,
-score + end positions) on MI355X, BASELINE.json config 2.
+"""Benchmark of the hot path: batched affine-gap alignment (GASAL2 kernels) and
+PairHMM on MI355X, BASELINE.json configs 1-5.  Default: config 2, SW local
+score + end positions over 1M pairs x 150 bp per GPU.
 
-A step = one pass of the HIP engine over one batch of 1M synthetic pairs
-(ql = tl = 150, SURVEY.md §8(d) generator, seed 0x5EED0002 + rank) that is
-already resident in HBM, launched through the C-ABI (gasalx_align_device) on
-torch's current stream.  Multi-GPU: one process per GPU, each aligns its own
-batch (weak scaling, no data-path collective); timing is bracketed by a
-barrier + synchronize and the max over ranks is reported.
+A step = one pass of the HIP engine over this rank's shard of one global
+synthetic batch (SURVEY.md §8(d) generator, gasalx_synth_range), already
+resident in HBM, launched through the C-ABI (gasalx_align_device) on a
+non-default stream; with N > 1 the step also all-gathers every rank's int32
+scores (RCCL over xGMI), the exchange step of SURVEY.md §8(e).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs P] [--workload sw_local|nw_tb|semi|pairhmm]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--pairs P]
+
+Multi-GPU: one process per GPU.  Under torchrun (WORLD_SIZE set) the ranks come
+from the environment; `--gpus N` without WORLD_SIZE starts N ranks itself
+(torch.distributed.run, 127.0.0.1) before any GPU call.  Timing is bracketed by
+a barrier + synchronize on both sides, the max over ranks is reported.
+
+After the timed steps every rank checks its shard's device outputs against the
+CPU oracle (oracle/, the reference's kernels restated in C), bit-exactly for
+integer outputs, rtol 1e-5 for PairHMM, and rank 0 checks the gathered scores;
+the line carries "parity".  At N = 1 the same oracle run is timed as the CPU
+baseline (the box's cores), beside a 1-core sample.
 """
 import argparse
 import dataclasses
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "genomics-gpu_amd"))
 import gasal_ffi as G  # noqa: E402
+import gasal_dist as D  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 instruction per 2 cycles (full-rate ops;
-# v_pk_*, max/min_32, perm, maximum3 issue at 4 — profiles/r01_valu_issue_rates.md)
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 2
+# VALU lane throughput: 256 CUs x 4 SIMDs x 16 lanes per clock x 2.4 GHz
+VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9            # 39.3 T int32 (or fp32) ops/s
+SIMDS, CLOCK = 256 * 4, 2.4e9
 
+MAIN_METRIC = "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %"
+
+# name: kind (synth config), pairs, scaling ("weak": pairs per GPU; "strong": global
+# pairs), params, algorithmic bytes per pair, algorithmic ops per cell, label
 WORKLOADS = {
-    # name: (synth kind, default pairs, params, algorithmic bytes per pair, int ops per cell, label)
-    "sw_local": (2, 1_000_000, dict(algo=G.LOCAL), 332, 12,
-                 "config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp, seed 0x5EED0002"),
-    "sw_local_start": (2, 1_000_000, dict(algo=G.LOCAL, start_pos=G.WITH_START), 340, 12,
-                       "config2 + WITH_START: SW local affine score+ends+starts, 1M pairs x 150bp, seed 0x5EED0002"),
-    "sw_local_tb": (2, 1_000_000, dict(algo=G.LOCAL, start_pos=G.WITH_TB), 340 + 152, 16,
-                    "config2 + WITH_TB: SW local affine score+ends+starts+CIGAR, 1M pairs x 150bp, seed 0x5EED0002"),
-    "nw_tb": (3, 100_000, dict(algo=G.GLOBAL, start_pos=G.WITH_TB), 650, 16,
-              "config3: NW global + traceback/CIGAR, 100K pairs x 300bp, seed 0x5EED0003"),
-    "semi": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), 364, 12,
-             "config4 shard: semi-global TARGET/TARGET, 150bp reads in 182bp windows, seed 0x5EED0004"),
-    "semi_start": (4, 1_250_000, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
-                                      max_query_len=192), 372, 12,
-                   "config4 shard + WITH_START: semi-global TARGET/TARGET score+ends+starts, 150bp reads in 182bp "
-                   "windows, seed 0x5EED0004"),
-    "pairhmm": (5, 100_000, None, 4762, 11,
-                "config5: PairHMM fp32 forward, 100K reads x haplotypes (250 x 500), seed 0x5EED0005"),
+    "sw_local": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL), bytes=332, ops=12,
+                     label="config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp per GPU, "
+                           "seed 0x5EED0002"),
+    "sw_local_start": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL, start_pos=G.WITH_START),
+                           bytes=340, ops=12,
+                           label="config2 + WITH_START: SW local score+ends+starts, 1M pairs x 150bp per GPU"),
+    "sw_local_tb": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL, start_pos=G.WITH_TB),
+                        bytes=340 + 152, ops=16,
+                        label="config2 + WITH_TB: SW local score+ends+starts+CIGAR, 1M pairs x 150bp per GPU"),
+    "nw_tb": dict(kind=3, pairs=100_000, scaling="weak", params=dict(algo=G.GLOBAL, start_pos=G.WITH_TB), bytes=650,
+                  ops=16, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
+    "semi": dict(kind=4, pairs=10_000_000, scaling="strong",
+                 params=dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), bytes=364, ops=12,
+                 label="config4: semi-global TARGET/TARGET, 10M 150bp reads in 182bp windows sharded over the "
+                       "GPUs, RCCL gather of scores, seed 0x5EED0004"),
+    "semi_start": dict(kind=4, pairs=10_000_000, scaling="strong",
+                       params=dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
+                                   max_query_len=192), bytes=372, ops=12,
+                       label="config4 + WITH_START: semi-global TARGET/TARGET score+ends+starts, 10M reads sharded"),
+    "semi_banded": dict(kind=4, pairs=10_000_000, scaling="strong", params=dict(algo=G.BANDED, k_band=16), bytes=364,
+                        ops=12, label="config4 data, banded-tiled k_band=16 (SURVEY §8(d) second run), 10M reads "
+                                      "sharded; cells = full rectangle"),
+    "pairhmm": dict(kind=5, pairs=100_000, scaling="weak", params=None, bytes=4762, ops=11,
+                    label="config5: PairHMM fp32 forward, 100K reads x haplotypes (250 x 500) per GPU, "
+                          "seed 0x5EED0005"),
+    "cpu_plumbing": dict(kind=1, pairs=1024, scaling="weak", params=dict(algo=G.LOCAL), bytes=152, ops=12,
+                         label="config1: 1024 pairs 64x64 SW local through the host-side CPU verify scorer "
+                               "(oracle/), same batch through the GPU, seed 0x5EED0001"),
 }
 METRICS = {
     "pairhmm": "GCUPS of PairHMM fp32 forward (config 5, 250x500) on MI355X",
+    "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
 }
+SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005}
 
 
-def synth_pairhmm(n, seed, rl=250, hl=500):
-    """haplotype 500 bp uniform; read = 250-bp substring with
-    2% mismatches; base quals U[10,40], insertion/deletion quals 45 (gcp ignored)."""
-    rng = np.random.default_rng(seed)
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=0,
+                    help="pairs per GPU (weak workloads) or global pairs (strong); default: the config's")
+    ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="1-core CPU baseline sample budget")
+    ap.add_argument("--parity-pairs", type=int, default=2_000_000,
+                    help="per rank: check at most this many pairs of the shard against the oracle (0 = none)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: leave out the all-gather of scores")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's shard of the global batch as a JSON line and exit (no GPU call)")
+    return ap.parse_args()
+
+
+# ----------------------------------------------------------------- launch ---
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`--gpus N` outside torchrun: run this script as N ranks (one process per GPU)
+    through torch.distributed.run, before this process touches the GPU, and exit
+    with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+# ------------------------------------------------------------------ data ----
+PH_BLOCK = 8192
+
+
+def synth_pairhmm(start, n, seed, rl=250, hl=500):
+    """SURVEY.md 8(d) config 5, pairs [start, start + n) of the global batch: haplotype
+    500 bp uniform; read = 250-bp substring with 2% mismatches; base quals U[10,40],
+    insertion/deletion quals 45 (gcp ignored).  Blocks of 8,192 pairs, each from
+    numpy's default_rng((seed, block)), so a rank generates only its shard."""
     alpha = np.frombuffer(b"ACGT", np.uint8)
-    haps = alpha[rng.integers(0, 4, (n, hl))]
-    start = rng.integers(0, hl - rl + 1, n)
-    reads = haps[np.arange(n)[:, None], start[:, None] + np.arange(rl)[None, :]].copy()
-    flip = rng.random((n, rl)) < 0.02
-    reads[flip] = alpha[(np.searchsorted(alpha, reads[flip]) + rng.integers(1, 4, int(flip.sum()))) % 4]
-    bq = rng.integers(10, 41, n * rl).astype(np.uint8)
+    reads, haps, bqs = [], [], []
+    b0, b1 = start // PH_BLOCK, (start + n + PH_BLOCK - 1) // PH_BLOCK
+    for b in range(b0, b1):
+        rng = np.random.default_rng((seed, b))
+        m = PH_BLOCK
+        hb = alpha[rng.integers(0, 4, (m, hl))]
+        st = rng.integers(0, hl - rl + 1, m)
+        rb = hb[np.arange(m)[:, None], st[:, None] + np.arange(rl)[None, :]].copy()
+        flip = rng.random((m, rl)) < 0.02
+        rb[flip] = alpha[(np.searchsorted(alpha, rb[flip]) + rng.integers(1, 4, int(flip.sum()))) % 4]
+        bq = rng.integers(10, 41, (m, rl)).astype(np.uint8)
+        lo, hi = max(start, b * PH_BLOCK) - b * PH_BLOCK, min(start + n, (b + 1) * PH_BLOCK) - b * PH_BLOCK
+        reads.append(rb[lo:hi]); haps.append(hb[lo:hi]); bqs.append(bq[lo:hi])
+    reads, haps, bq = np.concatenate(reads), np.concatenate(haps), np.concatenate(bqs).reshape(-1)
     iq = np.full(n * rl, 45, np.uint8)
     qm, de, xi, al = G.pairhmm_params(bq, iq, iq)
     return dict(reads=reads.reshape(-1), read_offsets=np.arange(n, dtype=np.uint32) * rl,
@@ -73,68 +153,120 @@ def synth_pairhmm(n, seed, rl=250, hl=500):
                 hap_offsets=np.arange(n, dtype=np.uint32) * hl, hap_lens=np.full(n, hl, np.uint32))
 
 
-def cpu_baseline_pairhmm(h, budget_s):
+def ph_subset(h, e):
+    """The first e pairs of a PairHMM batch (uniform lengths)."""
+    rl, hl = int(h["read_lens"][0]), int(h["hap_lens"][0])
+    out = {k: h[k][:e * rl] for k in ("reads", "qm", "delta", "xiksi", "alpha")}
+    out.update(haps=h["haps"][:e * hl], read_offsets=h["read_offsets"][:e], read_lens=h["read_lens"][:e],
+               hap_offsets=h["hap_offsets"][:e], hap_lens=h["hap_lens"][:e])
+    return out
+
+
+# ---------------------------------------------------------------- oracle ----
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    n = len(h["read_lens"])
-    chunk, done, cells, t_used = 2000, 0, 0, 0.0
-    while t_used < budget_s and done < n:
+    return O
+
+
+def oracle_threads():
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env > 0:
+        return env
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return min(16, n)   # one GPU's CPU share on the pool (16); the line records the host's total
+
+
+def host_info():
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "NUMA node(s)", "Socket(s)", "Thread(s) per core"):
+                info[k.strip().lower().replace(" ", "_").replace("(s)", "s")] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def oracle_align(O, batch, pkw, threads):
+    return O.align(batch, O.make_params(**pkw), n_threads=threads)
+
+
+def oracle_pairhmm(O, h, threads):
+    return O.pairhmm(h["reads"], h["read_offsets"], h["read_lens"], h["qm"], h["delta"], h["xiksi"], h["alpha"],
+                     h["haps"], h["hap_offsets"], h["hap_lens"], n_threads=threads)
+
+
+def cells_of(batch):
+    return int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
+
+
+def single_core_rate(O, kind, data, pkw, budget_s):
+    """The oracle on 1 thread over a prefix of the rank-0 shard, bounded by budget_s."""
+    chunk = 256 if kind == 5 else 4096
+    done, cells, used = 0, 0, 0.0
+    n = len(data["read_lens"]) if kind == 5 else data.n
+    while used < budget_s and done < n:
         e = min(done + chunk, n)
-        rl, hl = h["read_lens"][done:e], h["hap_lens"][done:e]
-        r0, h0 = int(h["read_offsets"][done]), int(h["hap_offsets"][done])
-        r1, h1 = int(h["read_offsets"][e - 1] + rl[-1]), int(h["hap_offsets"][e - 1] + hl[-1])
-        t0 = time.perf_counter()
-        O.pairhmm(h["reads"][r0:r1], h["read_offsets"][done:e] - r0, rl, h["qm"][r0:r1], h["delta"][r0:r1],
-                  h["xiksi"][r0:r1], h["alpha"][r0:r1], h["haps"][h0:h1], h["hap_offsets"][done:e] - h0, hl,
-                  n_threads=threads)
-        t_used += time.perf_counter() - t0
-        cells += int(np.sum(rl.astype(np.int64) * hl.astype(np.int64)))
+        if kind == 5:
+            sub = {k: (v[done * 250:e * 250] if k in ("reads", "qm", "delta", "xiksi", "alpha")
+                       else v[done * 500:e * 500] if k == "haps" else v[done:e]) for k, v in data.items()}
+            sub["read_offsets"] = sub["read_offsets"] - sub["read_offsets"][0]
+            sub["hap_offsets"] = sub["hap_offsets"] - sub["hap_offsets"][0]
+            t0 = time.perf_counter()
+            oracle_pairhmm(O, sub, 1)
+            used += time.perf_counter() - t0
+            cells += int(np.sum(sub["read_lens"].astype(np.int64) * sub["hap_lens"].astype(np.int64)))
+        else:
+            sub = data.slice(done, e)
+            t0 = time.perf_counter()
+            oracle_align(O, sub, pkw, 1)
+            used += time.perf_counter() - t0
+            cells += cells_of(sub)
         done = e
-    return {"value": round(cells / t_used / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"first {done} pairs of the rank-0 batch ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
-                      f"oracle/gasal_oracle.c orc_pairhmm_batch OpenMP x{threads}"}
+    return {"value": round(cells / used / 1e9, 4), "unit": "GCUPS", "cores": 1,
+            "sample": f"first {done} pairs of the rank-0 shard ({cells / 1e9:.3f} G cells, {used:.1f} s)"}
 
 
-def parse():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (default: the config's size)")
-    ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
-    ap.add_argument("--gather", action="store_true",
-                    help="N>1: all-gather every rank's int32 scores (RCCL) inside each timed step")
-    return ap.parse_args()
+# ---------------------------------------------------------------- parity ----
+def compare_align(g, o, fields, batch=None, cigar=False):
+    """Per-field mismatch counts between device results g and oracle results o.
+    CIGAR: n_ops for every pair; bytes for every pair whose CIGAR fits its pad8(ql)
+    slot and whose left neighbour's does too (an overflowing CIGAR runs
+    into the next slot, order-dependent in the reference)."""
+    mism = {f: int(np.count_nonzero(g[f] != o[f])) for f in fields}
+    extra = {}
+    if cigar:
+        mism["n_ops"] = int(np.count_nonzero(g["n_ops"] != o["n_ops"]))
+        slot = (batch.q_lens.astype(np.int64) + 7) // 8 * 8
+        over = o["n_ops"].astype(np.int64) > slot
+        ok = ~over
+        ok[1:] &= ~over[:-1]
+        gc, oc = g["cigar"], o["cigar"]
+        bad = 0
+        offs, nops = batch.q_offsets.astype(np.int64), o["n_ops"].astype(np.int64)
+        # vectorised byte compare over the checked pairs' CIGAR bytes
+        diff = np.flatnonzero(gc[:len(oc)] != oc)
+        if diff.size:
+            owner = np.searchsorted(offs, diff, side="right") - 1
+            rel = diff - offs[owner]
+            hit = ok[owner] & (rel < nops[owner])
+            bad = int(np.unique(owner[hit]).size)
+        mism["cigar_pairs"] = bad
+        extra["cigar_pairs_skipped_q14"] = int((~ok).sum())
+    return mism, extra
 
 
-def cpu_baseline(batch, params_kw, budget_s):
-    """The repo's CPU restatement of the GASAL2 kernels (oracle/), timed on a
-    bounded prefix of the same workload on this host's cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    op = O.make_params(**params_kw)
-    chunk = 20000
-    done_pairs, cells, t_used = 0, 0, 0.0
-    while t_used < budget_s and done_pairs < batch.n:
-        idx = np.arange(done_pairs, min(done_pairs + chunk, batch.n))
-        sub = batch.subset(idx)
-        t0 = time.perf_counter()
-        O.align(sub, op, n_threads=threads)
-        t_used += time.perf_counter() - t0
-        cells += int(np.sum(sub.q_lens.astype(np.int64) * sub.t_lens.astype(np.int64)))
-        done_pairs += len(idx)
-    return {"value": round(cells / t_used / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-            "sample": f"first {done_pairs} pairs of the rank-0 batch ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
-                      f"oracle/gasal_oracle.c OpenMP x{threads}"}
-
-
+# ------------------------------------------------------------------ e2e -----
 def end_to_end(eng, kind, data, params, cells, reps=5):
     """PCIe-inclusive rate through the host-buffer entry point (gasalx_align_host /
     gasalx_pairhmm_host): host arrays in, H2D + kernels + D2H, results back in host
@@ -166,8 +298,6 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
     res = {"value": round(cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_batch": round(dt * 1e3, 3),
            "ms_all": [round(t * 1e3, 3) for t in times], "path": path}
     if kind != 5 and params.start_pos == G.WITH_TB:
-        # the same call with a page-locked CIGAR buffer (as the reference's own host_res,
-        # res.cpp:8-70): the D2H skips the runtime's pageable staging copy
         host = G.PinnedHost(data.q_bytes)
         dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, cigar_out=host.array))
         host.close()
@@ -189,68 +319,156 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
     return res
 
 
+def dtype_label(plan, kind):
+    if kind == 5:
+        return "fp32"
+    if plan.startswith("wavefront16"):
+        return "int16x2 packed (exact value window), int32 fallback per declined block"
+    if plan.startswith("wavefront_"):
+        return "int32"
+    return "int32 (int16 row buffer, as the reference)"
+
+
+# ----------------------------------------------------------------- config 1 -
+def run_cpu_plumbing(args, wl):
+    """Config 1: the host-side CPU verify scorer over 1024 x 64x64 (timed K passes on
+    1 thread), and the same batch through the GPU, compared bit-exactly."""
+    O = _oracle()
+    import torch
+    n = args.pairs or wl["pairs"]
+    batch = G.Batch.synth(1, n, SEEDS[1])
+    pkw = wl["params"]
+    cells = cells_of(batch)
+    for _ in range(args.warmup):
+        oracle_align(O, batch, pkw, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        o = oracle_align(O, batch, pkw, 1)
+    dt = time.perf_counter() - t0
+    out = {"metric": METRICS["cpu_plumbing"], "value": round(cells * args.steps / dt / 1e9, 4), "unit": "GCUPS",
+           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "int32", "data": "synthetic (SURVEY.md 8(d) config 1 generator)",
+           "config": {"workload": wl["label"], "pairs": n, "cells_per_step": cells, "cores": 1}}
+    if torch.cuda.is_available():
+        eng = G.Engine(0)
+        g = eng.align_host(batch, G.make_params(**pkw), fields=["score", "q_end", "t_end"])
+        mism, _ = compare_align(g, o, ("score", "q_end", "t_end"))
+        out["parity"] = {"pairs_checked": n, "mismatches": sum(mism.values()), "by_field": mism,
+                         "against": "oracle/ (CPU restatement), same batch through gasalx_align_host",
+                         "plan": G.describe_plan(G.make_params(**pkw), 64, 64)}
+        eng.close()
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------ main ----
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus and args.gpus > 1:
+        spawn_ranks(args.gpus)
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    wl = WORKLOADS[args.workload]
+    if args.workload == "cpu_plumbing":
+        if world != 1:
+            sys.exit("bench.py: cpu_plumbing is a 1-process workload")
+        return run_cpu_plumbing(args, wl)
+
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+    kind, pkw = wl["kind"], wl["params"]
+    per = args.pairs or wl["pairs"]
+    n_global = per * world if wl["scaling"] == "weak" else per
+    seed = SEEDS[kind]
+    if kind == 5:
+        rl, hl = 250, 500
+    else:
+        rl, hl = G.synth_spec(kind)
+    shards = D.all_shards(n_global, rl, hl, world)
+    start, end = shards[rank]
+    n = end - start
+    counts = [e - s for s, e in shards]
+    do_gather = world > 1 and not args.no_gather
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local_rank, "pairs_global": n_global,
+                          "shard": [start, end], "gather": do_gather}), flush=True)
+        return
+
+    import torch
+    import torch.distributed as dist
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=dev)
 
-    kind, default_pairs, pkw, bytes_per_pair, ops_per_cell, label = WORKLOADS[args.workload]
-    n = args.pairs or default_pairs
-    seed = {2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005}[kind] + rank
     eng = G.Engine(local_rank)
     stream = torch.cuda.Stream(dev)      # a real (non-null) stream: kernels and timing events share it
     torch.cuda.set_stream(stream)
-    gathered = None
+    gather = D.ScoreGather(counts, world, dev, dtype=torch.float32 if kind == 5 else torch.int32) \
+        if do_gather else None
+    t_syn = time.perf_counter()
     if kind == 5:
-        h = synth_pairhmm(n, seed)
+        h = synth_pairhmm(start, n, seed)
+        data = h
         cells_per_step = int(np.sum(h["read_lens"].astype(np.int64) * h["hap_lens"].astype(np.int64)))
         dh = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.int32) if v.dtype == np.uint32 else v).to(dev)
               for k, v in h.items()}
-        result = torch.empty(n, dtype=torch.float32, device=dev)
+        result = gather.buf if gather else torch.empty(max(n, 1), dtype=torch.float32, device=dev)
         hptrs = {k: v.data_ptr() for k, v in dh.items()}
-        maxr, maxh = int(h["read_lens"].max()), int(h["hap_lens"].max())
-        plan = f"pairhmm_wavefront (read {maxr} x hap {maxh})"
+        plan = f"pairhmm_wavefront (read {rl} x hap {hl})"
 
-        def step():
-            eng.pairhmm_device_ptrs(hptrs, len(h["reads"]), len(h["haps"]), n, maxr, maxh, result.data_ptr(),
+        def align():
+            eng.pairhmm_device_ptrs(hptrs, len(h["reads"]), len(h["haps"]), n, rl, hl, result.data_ptr(),
                                     stream.cuda_stream)
-    else:
-        batch = G.Batch.synth(kind, n, seed)
-        cells_per_step = int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
-        params = G.make_params(**pkw)
 
-        # inputs resident in HBM before the timed region
+        def results():
+            return {"result": result[:n].cpu().numpy()}
+    else:
+        batch = G.Batch.synth(kind, n, seed, start=start)
+        data = batch
+        cells_per_step = cells_of(batch)
+        params = G.make_params(**pkw)
         as_i32 = lambda a: torch.from_numpy(a.view(np.int32).copy()).to(dev)
-        d = {
-            "q_batch": torch.from_numpy(batch.q_data).to(dev), "t_batch": torch.from_numpy(batch.t_data).to(dev),
-            "q_offsets": as_i32(batch.q_offsets), "t_offsets": as_i32(batch.t_offsets),
-            "q_lens": as_i32(batch.q_lens), "t_lens": as_i32(batch.t_lens),
-            "aln_score": torch.empty(n, dtype=torch.int32, device=dev),
-        }
+        d = {"q_batch": torch.from_numpy(batch.q_data).to(dev), "t_batch": torch.from_numpy(batch.t_data).to(dev),
+             "q_offsets": as_i32(batch.q_offsets), "t_offsets": as_i32(batch.t_offsets),
+             "q_lens": as_i32(batch.q_lens), "t_lens": as_i32(batch.t_lens),
+             "aln_score": gather.buf if gather else torch.empty(n, dtype=torch.int32, device=dev)}
+        fields = ["score"]
         if pkw["algo"] != G.GLOBAL:
             d["q_end"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_end"] = torch.empty(n, dtype=torch.int32, device=dev)
+            fields += ["q_end", "t_end"]
         if pkw.get("start_pos") in (G.WITH_START, G.WITH_TB) and pkw["algo"] != G.GLOBAL:
             d["q_start"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_start"] = torch.empty(n, dtype=torch.int32, device=dev)
-        if pkw.get("start_pos") == G.WITH_TB:
+            fields += ["q_start", "t_start"]
+        tb = pkw.get("start_pos") == G.WITH_TB
+        if tb:
             d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
             d["n_cigar_ops"] = torch.empty(n, dtype=torch.int32, device=dev)
         ptrs = {k: v.data_ptr() for k, v in d.items()}
-        maxq, maxt = int(batch.q_lens.max()), int(batch.t_lens.max())
-        plan = G.describe_plan(params, maxq, maxt)
-        gathered = [torch.empty_like(d["aln_score"]) for _ in range(world)] if (args.gather and world > 1) else None
+        plan = G.describe_plan(params, rl, hl)
+        names = {"score": "aln_score", "q_end": "q_end", "t_end": "t_end", "q_start": "q_start",
+                 "t_start": "t_start"}
 
-        def step():
-            eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, maxq, maxt, stream.cuda_stream)
-            if gathered is not None:   # optional exchange step of SURVEY §8(e): every rank gets all scores
-                dist.all_gather(gathered, d["aln_score"])
+        def align():
+            eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, rl, hl, stream.cuda_stream)
+
+        def results():
+            r = {f: d[names[f]][:n].cpu().numpy() for f in fields}
+            if tb:
+                r["cigar"] = d["cigar"].cpu().numpy()
+                r["n_ops"] = d["n_cigar_ops"].cpu().numpy().view(np.uint32)
+            return r
+    torch.cuda.synchronize(dev)
+    synth_s = time.perf_counter() - t_syn
+
+    def step():
+        align()
+        if gather is not None:       # the exchange step of SURVEY §8(e): every rank gets all scores
+            gather()
 
     for _ in range(args.warmup):
         step()
@@ -258,29 +476,97 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
         ev[i][0].record(stream)
-        step()
+        align()
         ev[i][1].record(stream)
+        if gather is not None:
+            gather()
+        ev[i][2].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    gath_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    t = torch.tensor([elapsed, kern_ms, gath_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms, gath_ms = (float(x) for x in t)
+
+    # ---- parity: this rank's shard against the oracle (the CPU baseline at N = 1) ----
+    parity, cpu = None, None
+    O = _oracle() if (args.parity_pairs > 0 or (world == 1 and not args.no_cpu)) else None
+    threads = oracle_threads()
+    if args.parity_pairs > 0:
+        m = min(n, args.parity_pairs)
+        got = results()
+        t_o = time.perf_counter()
+        if kind == 5:
+            ref = oracle_pairhmm(O, ph_subset(data, m), threads)
+            g_ = got["result"][:m]
+            rel = np.abs(g_.astype(np.float64) - ref) / np.maximum(np.abs(ref.astype(np.float64)), 1e-30)
+            mism = {"result_rtol_1e-5": int(np.count_nonzero(~(rel <= 1e-5)))}
+            extra = {"max_rel_err": float(rel.max(initial=0.0))}
+            ref_scores = ref
+        else:
+            sub = data.slice(0, m)
+            ref = oracle_align(O, sub, pkw, threads)
+            gsub = {f: got[f][:m] for f in fields}
+            if tb:
+                gsub["cigar"] = got["cigar"][:sub.q_bytes]
+                gsub["n_ops"] = got["n_ops"][:m]
+            mism, extra = compare_align(gsub, ref, fields, batch=sub, cigar=tb)
+            ref_scores = ref["score"]
+        oracle_s = time.perf_counter() - t_o
+        cells_checked = (m * rl * hl)
+        tot = torch.tensor([m, sum(mism.values())], dtype=torch.int64, device=dev)
+        gather_bad = 0
+        if gather is not None:
+            # the gathered scores (timed steps' exchange) against every rank's oracle scores
+            og = D.ScoreGather(counts, world, dev, dtype=gather.buf.dtype)
+            og.buf[:m] = torch.as_tensor(np.asarray(ref_scores), device=dev)
+            og()
+            gfull = gather.out.cpu().numpy()
+            ofull = og.out.cpu().numpy()
+            mlist = [min(c, args.parity_pairs) for c in counts]
+            for r in range(world):
+                a, b = gfull[r, :mlist[r]], ofull[r, :mlist[r]]
+                if kind == 5:
+                    rr = np.abs(a.astype(np.float64) - b) / np.maximum(np.abs(b.astype(np.float64)), 1e-30)
+                    gather_bad += int(np.count_nonzero(~(rr <= 1e-5)))
+                else:
+                    gather_bad += int(np.count_nonzero(a != b))
+        if world > 1:
+            dist.all_reduce(tot)
+        parity = {"pairs_checked": int(tot[0]), "mismatches": int(tot[1]),
+                  "by_field_rank0": mism, **extra,
+                  "tolerance": "rtol 1e-5" if kind == 5 else "bit-exact",
+                  "against": "oracle/ (CPU restatement of the reference kernels), on the timed steps' outputs"}
+        if gather is not None:
+            parity["gathered_scores_checked"] = int(sum(min(c, args.parity_pairs) for c in counts))
+            parity["gathered_mismatches"] = gather_bad
+        if world == 1 and not args.no_cpu:
+            cpu = {"value": round(cells_checked / oracle_s / 1e9, 4), "unit": "GCUPS", "cores": threads,
+                   "kind": "port",
+                   "sample": f"first {m} pairs of the rank-0 batch ({cells_checked / 1e9:.2f} G cells, "
+                             f"{oracle_s:.1f} s, the parity run), oracle/gasal_oracle.c OpenMP x{threads}"}
+    if world == 1 and not args.no_cpu:
+        if cpu is None:
+            cpu = {"value": None, "unit": "GCUPS", "cores": threads, "kind": "port", "sample": "parity run skipped"}
+        cpu["single_core"] = single_core_rate(O, kind, data, pkw, args.cpu_seconds)
+        cpu["host"] = host_info()
+        cpu["note"] = (f"cores = the OpenMP threads used (OMP_NUM_THREADS, else min(16, CPUs)): one GPU's "
+                       f"CPU share on this pool; host totals in 'host'")
 
     if rank == 0:
-        total_cells = cells_per_step * world * args.steps
-        gcups = total_cells / elapsed / 1e9
+        total_cells = n_global * rl * hl        # every pair of every shard (uniform lengths)
+        gcups = total_cells * args.steps / elapsed / 1e9
         kern_s = kern_ms / 1e3
-        achieved = bytes_per_pair * n / kern_s / 1e9
-        valu_roof = None
+        achieved = wl["bytes"] * n / kern_s / 1e9
         pmc = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
         if os.path.exists(pmc_path):
@@ -288,16 +574,24 @@ def main():
                 pmc = json.load(open(pmc_path))
             except Exception:
                 pmc = None
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-        if pmc and pmc.get("valu_insts_per_launch") and pmc.get("pairs_per_launch", n) == n:
-            # dynamic VALU wave-instructions of the dominant kernel (SQ_INSTS_VALU, same workload)
-            ach = pmc["valu_insts_per_launch"] / kern_s
-            valu_roof = {"bound": "valu-issue", "achieved": round(ach / 1e12, 4), "peak": VALU_PEAK_WAVE_INSTR / 1e12,
-                         "unit": "T wave-instr/s", "frac": round(ach / VALU_PEAK_WAVE_INSTR, 4),
-                         "valu_insts_per_launch": pmc["valu_insts_per_launch"],
-                         "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU)"}
+        same = pmc is not None and pmc.get("pairs_per_launch") == n
+        traffic = pmc.get("hbm_bytes_per_launch") if same else None
+        packed = kind == 5 or plan.startswith("wavefront16")
+        lane_rate = VALU_LANE_OPS * (2 if packed else 1)
+        peak_cells = lane_rate / wl["ops"]
+        kcells = cells_per_step / kern_s
+        valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
+                "unit": "T cells/s", "frac": round(kcells / peak_cells, 4), "ops_per_cell": wl["ops"],
+                "basis": (f"SURVEY.md 8(d) algorithmic ops per cell at "
+                          f"{'packed 2x16-bit / 2xfp32' if packed else 'int32'} VALU lane rate "
+                          f"{lane_rate / 1e12:.1f} T ops/s")}
+        if same and pmc.get("valu_insts_per_launch"):
+            valu["issue"] = {"valu_wave_instr_per_launch": pmc["valu_insts_per_launch"],
+                             "cycles_per_valu_instr_per_simd":
+                                 round(SIMDS * CLOCK * kern_s / pmc["valu_insts_per_launch"], 3),
+                             "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU)"}
         out = {
-            "metric": METRICS.get(args.workload, "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %"),
+            "metric": METRICS.get(args.workload, MAIN_METRIC),
             "value": round(gcups, 2),
             "unit": "GCUPS",
             "n_gpus": world,
@@ -305,31 +599,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl["scaling"],
             "vs_baseline": None,
-            "dtype": "fp32" if kind == 5 else "int32",
-            "data": "synthetic (SURVEY.md 8(d) generator, std::mt19937_64), resident in HBM",
-            "config": {"workload": label, "pairs_per_gpu": n, "cells_per_gpu_step": cells_per_step,
-                       "plan": plan,
-                       "parallelism": f"dp{world} (pairs sharded)" + (", all-gather of scores" if gathered else "")},
+            "dtype": dtype_label(plan, kind),
+            "data": "synthetic (SURVEY.md 8(d) generator), resident in HBM",
+            "config": {"workload": wl["label"], "pairs_global": n_global, "pairs_rank0": n,
+                       "cells_rank0_step": cells_per_step, "plan": plan,
+                       "parallelism": f"dp{world} (cell-balanced contiguous shards of one global batch)" +
+                                      (", RCCL all-gather of scores in every step" if gather else ""),
+                       "synth_s_rank0": round(synth_s, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "bytes_per_pair": bytes_per_pair, "kernel_ms": round(kern_ms, 4),
-                         "timed": "HIP events around the whole step on its stream (every kernel of the step; "
-                                  "WITH_START/WITH_TB steps launch more than the dominant kernel)"},
-            "valu_roofline": valu_roof,
+                         "bytes_per_pair": wl["bytes"], "kernel_ms": round(kern_ms, 4),
+                         "timed": "HIP events around the align call on its stream (every kernel of the call; "
+                                  "WITH_START/WITH_TB calls launch more than the dominant kernel)"},
+            "valu_roofline": valu,
             "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
+            "gather_ms": round(gath_ms, 4) if gather else None,
+            "parity": parity,
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
         if world == 1 and not args.no_e2e:
-            out["end_to_end"] = end_to_end(eng, kind, h if kind == 5 else batch, None if kind == 5 else params,
-                                           cells_per_step)
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = (cpu_baseline_pairhmm(h, args.cpu_seconds) if kind == 5
-                                   else cpu_baseline(batch, pkw, args.cpu_seconds))
+            out["end_to_end"] = end_to_end(eng, kind, data, None if kind == 5 else params, cells_per_step)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
+    eng.close()
     if world > 1:
         dist.destroy_process_group()
+    if parity and (parity["mismatches"] or parity.get("gathered_mismatches")):
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -3,10 +3,15 @@
 Pairs are independent, so a batch is split into contiguous ranges of pairs
 with (nearly) equal cell counts — the prefix sum of ql·tl — one range per
 rank (one process per GPU).  Each rank aligns its range with its own engine;
-no collective is on the data path.  The optional exchange step is one
-all-gather of the per-pair int32 results (RCCL over xGMI with the "nccl"
-backend on GPUs, gloo on CPU), replacing the reference's per-thread host
-result buffers (test_prog.cpp:203-231) with a node-wide result array.
+no collective is on the data path.  The exchange step is one all-gather of the
+per-pair int32 results (RCCL over xGMI with the "nccl" backend on GPUs, gloo on
+CPU for tests), replacing the reference's per-thread host result buffers
+(test_prog.cpp:203-231) with a node-wide result array.
+
+The same functions serve bench.py (engine on the GPU, RCCL) and the world-size-2
+gloo test (oracle as the aligner): `rank_shard` picks the rank's range of one
+global batch, `synth_shard` generates exactly those pairs (gasalx_synth_range),
+`ScoreGather` is the exchange step the bench times inside every step.
 """
 from __future__ import annotations
 
@@ -40,48 +45,80 @@ def shard_bounds(cells: np.ndarray, world: int) -> list[tuple[int, int]]:
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
 
 
+def rank_shard(q_lens, t_lens, rank: int, world: int) -> tuple[int, int]:
+    """This rank's [start, end) of a global batch with these lengths."""
+    return shard_bounds(cell_counts(q_lens, t_lens), world)[rank]
+
+
 def shard_batch(batch, rank: int, world: int):
-    """This rank's pairs as a freshly packed Batch, plus its [start, end)."""
-    start, end = shard_bounds(cell_counts(batch.q_lens, batch.t_lens), world)[rank]
-    return batch.subset(np.arange(start, end)), start, end
+    """This rank's pairs as a batch (a view when the layout allows), plus its [start, end)."""
+    start, end = rank_shard(batch.q_lens, batch.t_lens, rank, world)
+    return batch.slice(start, end), start, end
+
+
+def synth_shard(kind: int, n_global: int, seed: int, rank: int, world: int):
+    """This rank's shard of the seeded synthetic global batch of n_global pairs
+    (SURVEY.md §8(d) configs 1-4), generated on its own: (batch, start, end)."""
+    import gasal_ffi as G
+    ql, tl = G.synth_spec(kind)
+    start, end = rank_shard(np.full(n_global, ql), np.full(n_global, tl), rank, world)
+    return G.Batch.synth(kind, end - start, seed, start=start), start, end
+
+
+def all_shards(n_global: int, q_len: int, t_len: int, world: int) -> list[tuple[int, int]]:
+    return shard_bounds(cell_counts(np.full(n_global, q_len), np.full(n_global, t_len)), world)
+
+
+class ScoreGather:
+    """The exchange step: every rank's per-pair int32 (or fp32) results, padded to the
+    largest shard (all_gather needs equal shapes), gathered into one [world, cap]
+    tensor on every rank.  `buf` is the rank's padded result tensor; the aligner
+    writes its first n_local entries in place."""
+
+    def __init__(self, counts: list[int], world: int, device, dtype=None):
+        import torch
+        self.counts = list(counts)
+        self.world = world
+        self.cap = max(max(self.counts), 1)
+        dt = dtype or torch.int32
+        self.buf = torch.zeros(self.cap, dtype=dt, device=device)
+        self.out = torch.zeros((world, self.cap), dtype=dt, device=device)
+        self._parts = list(self.out.unbind(0))
+
+    def __call__(self):
+        import torch.distributed as dist
+        dist.all_gather(self._parts, self.buf)
+
+    def full(self) -> np.ndarray:
+        """The gathered results in global pair order (padding dropped)."""
+        h = self.out.cpu().numpy()
+        return np.concatenate([h[r, :self.counts[r]] for r in range(self.world)])
 
 
 def gather_results(local: dict, start: int, end: int, n_total: int, world: int, device="cpu",
                    fields=("score", "q_end", "t_end")) -> dict:
-    """All-gather per-pair int32 results of every rank into full arrays.
-
-    Shards have unequal sizes; each rank pads its slice to the largest shard
-    (all_gather needs equal shapes) and the padding is dropped after."""
+    """All-gather per-pair int32 results of every rank into full arrays."""
     import torch
     import torch.distributed as dist
     sizes = torch.tensor([end - start], dtype=torch.int64, device=device)
     all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
     dist.all_gather(all_sizes, sizes)
     counts = [int(s.item()) for s in all_sizes]
-    cap = max(max(counts), 1)
-    nf = len(fields)
-    buf = torch.zeros((nf, cap), dtype=torch.int32, device=device)
-    for i, f in enumerate(fields):
-        buf[i, :end - start] = torch.as_tensor(np.asarray(local[f], np.int32), device=device)
-    out = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf)
-    full = {f: np.empty(n_total, np.int32) for f in fields}
-    pos = 0
-    for r in range(world):
-        part = out[r].cpu().numpy()
-        for i, f in enumerate(fields):
-            full[f][pos:pos + counts[r]] = part[i, :counts[r]]
-        pos += counts[r]
-    if pos != n_total:
-        raise RuntimeError(f"gathered {pos} pairs, expected {n_total}")
+    full = {}
+    for f in fields:
+        g = ScoreGather(counts, world, device)
+        g.buf[:end - start] = torch.as_tensor(np.asarray(local[f], np.int32), device=device)
+        g()
+        full[f] = g.full()
+    if len(full[fields[0]]) != n_total:
+        raise RuntimeError(f"gathered {len(full[fields[0]])} pairs, expected {n_total}")
     return full
 
 
 def align_sharded(align_fn, batch, params, rank: int, world: int, gather: bool = True, device="cpu",
                   fields=("score", "q_end", "t_end")):
     """Shard `batch`, align this rank's part with align_fn(sub_batch, params) -> dict,
-    and (optionally) all-gather the results.  align_fn is the engine's align_host
-    (or align_device wrapper) in production."""
+    and (optionally) all-gather the results."""
     sub, start, end = shard_batch(batch, rank, world)
     local = align_fn(sub, params) if sub.n else {f: np.zeros(0, np.int32) for f in fields}
     if not gather:

@@ -29,7 +29,7 @@ EXPORTS = (
     "gasalx_abi_version", "gasalx_last_error", "gasalx_device_count", "gasalx_engine_create",
     "gasalx_engine_destroy", "gasalx_align_device", "gasalx_align_host", "gasalx_describe_plan",
     "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
-    "gasalx_synth_pairs",
+    "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range",
 )
 
 
@@ -138,15 +138,33 @@ class Batch:
         return cls(qd, qo, ql, td, to, tl)
 
     @classmethod
-    def synth(cls, kind: int, n: int, seed: int):
-        """SURVEY.md §8(d) workloads (kind 1..4 = configs 1..4), via gasalx_synth_pairs."""
+    def synth(cls, kind: int, n: int, seed: int, start: int = 0):
+        """SURVEY.md §8(d) workloads (kind 1..4 = configs 1..4): pairs [start, start + n)
+        of the seeded batch, via gasalx_synth_range (offsets start at 0)."""
         qb, tb = ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib().gasalx_synth_sizes(kind, ctypes.c_uint32(n), ctypes.byref(qb), ctypes.byref(tb)), "synth_sizes")
         qd, td = np.zeros(qb.value, np.uint8), np.zeros(tb.value, np.uint8)
         qo, ql, to, tl = (np.zeros(n, np.uint32) for _ in range(4))
-        _check(lib().gasalx_synth_pairs(kind, ctypes.c_uint64(seed), ctypes.c_uint32(n), _p(qd), _p(qo), _p(ql),
-                                        _p(td), _p(to), _p(tl)), "synth_pairs")
+        _check(lib().gasalx_synth_range(kind, ctypes.c_uint64(seed), ctypes.c_uint64(start), ctypes.c_uint32(n),
+                                        _p(qd), _p(qo), _p(ql), _p(td), _p(to), _p(tl)), "synth_range")
         return cls(qd, qo, ql, td, to, tl)
+
+    def slice(self, start: int, end: int):
+        """Pairs [start, end) as a batch of their own.  When the pairs' bytes are laid out
+        in order (offsets increasing, each sequence in its own padded slot, as
+        gasal_host_batch_fill writes them) this is a view with rebased offsets;
+        otherwise the pairs are re-packed (subset)."""
+        if end <= start:
+            return self.subset([])
+        qo, to = self.q_offsets[start:end].astype(np.int64), self.t_offsets[start:end].astype(np.int64)
+        ql, tl = self.q_lens[start:end].astype(np.int64), self.t_lens[start:end].astype(np.int64)
+        qp, tp = (ql + 7) // 8 * 8, (tl + 7) // 8 * 8
+        if np.array_equal(qo[1:], qo[:-1] + qp[:-1]) and np.array_equal(to[1:], to[:-1] + tp[:-1]):
+            q0, t0 = int(qo[0]), int(to[0])
+            q1, t1 = int(qo[-1] + qp[-1]), int(to[-1] + tp[-1])
+            return Batch(self.q_data[q0:q1], (qo - q0).astype(np.uint32), self.q_lens[start:end].copy(),
+                         self.t_data[t0:t1], (to - t0).astype(np.uint32), self.t_lens[start:end].copy())
+        return self.subset(np.arange(start, end))
 
     def subset(self, idx):
         """Re-pack pairs idx into a fresh batch (keeps each pair's padded bytes)."""
@@ -271,6 +289,13 @@ class Engine:
                        g("haps"), g("hap_offsets"), g("hap_lens"), read_bytes, hap_bytes, n, max_r, max_h)
         _check(lib().gasalx_pairhmm_device(self._h, ctypes.byref(hb), ctypes.c_void_p(result_ptr),
                                            ctypes.c_void_p(stream or None)), "pairhmm_device")
+
+
+def synth_spec(kind: int):
+    """(query length, target length) of a synthetic workload (all pairs alike)."""
+    q, t = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().gasalx_synth_spec(kind, ctypes.byref(q), ctypes.byref(t)), "synth_spec")
+    return q.value, t.value
 
 
 def describe_plan(params: Params, max_q: int, max_t: int) -> str:

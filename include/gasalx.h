@@ -149,10 +149,17 @@ int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *d
 
 /* Synthetic workloads of SURVEY.md §8(d) (benchmark/test data, std::mt19937_64).
  * Writes a GASAL2-layout batch (N_CODE padding) into caller buffers sized by
- * gasalx_synth_sizes.  kind: 1..4 = configs 1..4. */
+ * gasalx_synth_sizes.  kind: 1..4 = configs 1..4.  Pairs come in blocks of 65,536,
+ * each from its own seeded generator (block 0: `seed` itself), so
+ * gasalx_synth_range can write pairs [start, start + n) of a larger batch on
+ * their own (one rank's shard); offsets then start at 0. */
 int gasalx_synth_sizes(int kind, uint32_t n_pairs, uint64_t *q_bytes, uint64_t *t_bytes);
+int gasalx_synth_spec(int kind, uint32_t *q_len, uint32_t *t_len);
 int gasalx_synth_pairs(int kind, uint64_t seed, uint32_t n_pairs, uint8_t *q_batch, uint32_t *q_offsets,
                        uint32_t *q_lens, uint8_t *t_batch, uint32_t *t_offsets, uint32_t *t_lens);
+int gasalx_synth_range(int kind, uint64_t seed, uint64_t start, uint32_t n_pairs, uint8_t *q_batch,
+                       uint32_t *q_offsets, uint32_t *q_lens, uint8_t *t_batch, uint32_t *t_offsets,
+                       uint32_t *t_lens);
 
 #ifdef __cplusplus
 }

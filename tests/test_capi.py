@@ -106,3 +106,25 @@ def test_no_gpu_call_fails_loudly_without_device():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         G.Engine(0)
+
+
+def test_synth_range_is_a_shard_of_the_global_batch():
+    # pairs [start, start + n) generated alone equal the same pairs of the whole batch,
+    # across a 65,536-pair block boundary (gasalx_synth_range: one generator per block)
+    full = G.Batch.synth(1, 70000, 0x5EED0001)
+    for start, n in ((0, 5), (65530, 12), (69990, 10)):
+        part = G.Batch.synth(1, n, 0x5EED0001, start=start)
+        sl = full.slice(start, start + n)
+        assert np.array_equal(part.q_data, sl.q_data) and np.array_equal(part.t_data, sl.t_data)
+        assert np.array_equal(part.q_offsets, sl.q_offsets) and np.array_equal(part.t_lens, sl.t_lens)
+    assert G.synth_spec(4) == (150, 182) and G.synth_spec(1) == (64, 64)
+
+
+def test_batch_slice_matches_subset():
+    b = G.Batch.from_pairs(["ACGTA", "A" * 17, "CG", "T" * 8], ["GG", "C" * 9, "ACGTACGTA", "A"])
+    for s, e in ((0, 4), (1, 3), (2, 2), (3, 4)):
+        x, y = b.slice(s, e), b.subset(np.arange(s, e))
+        assert x.n == y.n
+        if x.n:
+            assert np.array_equal(x.q_data, y.q_data) and np.array_equal(x.t_offsets, y.t_offsets)
+            assert np.array_equal(x.q_lens, y.q_lens)

@@ -70,3 +70,34 @@ def test_gloo_world2_sharded_align_and_gather(tmp_path):
         got = np.load(tmp_path / f"r{r}.npz")
         for f in ("score", "q_end", "t_end"):
             assert np.array_equal(got[f], ref[f]), (r, f)
+
+
+def _bench_path_worker(rank, world, port, out_dir, kind, n_global):
+    """The bench's multi-GPU step on CPU: this rank's shard of one global synthetic
+    batch (gasal_dist.synth_shard -> gasalx_synth_range), aligned (here by the oracle,
+    on the GPU by the engine into ScoreGather.buf), then the exchange step
+    (ScoreGather, the same all_gather the bench times in every step)."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ql, tl = G.synth_spec(kind)
+    shards = D.all_shards(n_global, ql, tl, world)
+    sub, start, end = D.synth_shard(kind, n_global, 0x5EED0000 + kind, rank, world)
+    assert (start, end) == shards[rank] and sub.n == end - start
+    gat = D.ScoreGather([e - s for s, e in shards], world, "cpu")
+    local = O.align(sub, O.make_params(algo=O.LOCAL), n_threads=1)
+    gat.buf[:sub.n] = torch.from_numpy(local["score"])
+    gat()
+    np.save(os.path.join(out_dir, f"g{rank}.npy"), gat.full())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind,n_global", [(2, 1, 701), (3, 2, 257)])
+def test_gloo_bench_shard_path(tmp_path, world, kind, n_global):
+    O.build()
+    mp.spawn(_bench_path_worker, args=(world, _free_port(), str(tmp_path), kind, n_global), nprocs=world, join=True)
+    full = G.Batch.synth(kind, n_global, 0x5EED0000 + kind)
+    ref = O.align(full, O.make_params(algo=O.LOCAL))["score"]
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"g{r}.npy"), ref), r

@@ -648,3 +648,33 @@ def test_local_global_every_packed_shape(engine, monkeypatch, algo, g, r):
         plan = G.describe_plan(G.make_params(**kw), ql, 240)
         assert plan == f"wavefront16_{'local' if algo == G.LOCAL else 'global'}_G{g}R{r}", plan
         check(engine, b, **kw)
+
+
+# ------------------------------------------- config 1 and the second oracle ----
+def test_config1_through_gpu(engine):
+    """BASELINE config 1 (1024 pairs 64x64, seed 0x5EED0001): the batch the CPU verify
+    scorer runs (tests/test_independent.py) through the GPU, against both restatements."""
+    import independent as I
+    b = G.Batch.synth(1, 1024, 0x5EED0001)
+    g, o = check(engine, b, algo=G.LOCAL)
+    r = I.local(b)
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(g[f], r[f]), f
+
+
+@pytest.mark.parametrize("head,tail", [(0, 0), (0, 2), (1, 3), (2, 2), (3, 1)])
+def test_gpu_against_independent_restatement(engine, head, tail):
+    import independent as I
+    rng = np.random.default_rng(0x1D + 4 * head + tail)
+    qs, ts = helpers.random_pairs(rng, 400, 1, 120, 1, 160, alphabet=b"ACGTN")
+    b = G.Batch.from_pairs(qs, ts)
+    g = engine.align_host(b, G.make_params(algo=G.SEMI_GLOBAL, head=head, tail=tail))
+    r = I.semi(b, head, tail)
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(g[f], r[f]), f
+    g = engine.align_host(b, G.make_params(algo=G.LOCAL, second_best=1))
+    r = I.local(b, second=True)
+    for f in ("score", "q_end", "t_end", "score2", "q_end2", "t_end2"):
+        assert np.array_equal(g[f], r[f]), f
+    g = engine.align_host(b, G.make_params(algo=G.GLOBAL))
+    assert np.array_equal(g["score"], I.global_(b)["score"])
