@@ -32,6 +32,10 @@ import sys
 import time
 
 import numpy as np
+# torch first: its bundled HIP runtime (soname libamdhip64.so.7) must be the one
+# libgasal binds to; loading libgasal first would bring in /opt/rocm's copy as well,
+# and two HIP runtimes in one process do not share the device
+import torch  # noqa: F401
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "genomics-gpu_amd"))
@@ -334,7 +338,6 @@ def run_cpu_plumbing(args, wl):
     """Config 1: the host-side CPU verify scorer over 1024 x 64x64 (timed K passes on
     1 thread), and the same batch through the GPU, compared bit-exactly."""
     O = _oracle()
-    import torch
     n = args.pairs or wl["pairs"]
     batch = G.Batch.synth(1, n, SEEDS[1])
     pkw = wl["params"]
@@ -396,7 +399,6 @@ def main():
                           "shard": [start, end], "gather": do_gather}), flush=True)
         return
 
-    import torch
     import torch.distributed as dist
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)

@@ -442,4 +442,23 @@ int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *d
     return GASALX_OK;
 }
 
+int gasalx_host_alloc(uint64_t bytes, void **out) {
+    if (!out) { gx::set_error("gasalx_host_alloc: null output"); return GASALX_EINVAL; }
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        gx::set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        return GASALX_ENOMEM;
+    }
+    return GASALX_OK;
+}
+
+int gasalx_host_free(void *p) {
+    if (!p) return GASALX_OK;
+    hipError_t e = hipHostFree(p);
+    if (e != hipSuccess) { gx::set_error(std::string("hipHostFree: ") + hipGetErrorString(e)); return GASALX_EDEVICE; }
+    return GASALX_OK;
+}
+
 }  // extern "C"

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -29,7 +30,7 @@ EXPORTS = (
     "gasalx_abi_version", "gasalx_last_error", "gasalx_device_count", "gasalx_engine_create",
     "gasalx_engine_destroy", "gasalx_align_device", "gasalx_align_host", "gasalx_describe_plan",
     "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
-    "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range",
+    "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
 )
 
 
@@ -181,35 +182,34 @@ SENTINEL = -(2 ** 31) + 7
 OUT_FIELDS = ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2", "t_end2")
 
 
+class _PinnedArray(np.ndarray):
+    """ndarray over page-locked bytes; holds its PinnedHost so the memory lives as
+    long as any view of it does."""
+    _owner = None
+
+
 class PinnedHost:
-    """Page-locked host bytes from the engine's own HIP runtime (hipHostMalloc in the
-    libamdhip64 libgasal links; torch ships a second runtime whose pinned pages this
-    one would treat as pageable).  For caller-owned result buffers such as
-    align_host(cigar_out=...), as the reference's host_res is pinned (res.cpp:8-70).
-    `array` is valid until close()."""
+    """Page-locked host bytes from libgasal's own HIP runtime (gasalx_host_alloc), for
+    caller-owned buffers such as align_host(cigar_out=...), as the reference's host_res
+    is pinned (res.cpp:8-70).
+
+    `array` (and every view or slice of it) keeps this object alive, and the memory
+    is freed only when the last of them is gone: close() drops this handle's own
+    reference, it never frees memory an array still points at."""
 
     def __init__(self, nbytes: int):
-        lib()
-        self._p = None
-        # the soname libgasal.so records (ldd: libamdhip64.so.7 on ROCm 7), already loaded
-        self._hip = ctypes.CDLL("libamdhip64.so.7")
+        L = lib()
         self._p = ctypes.c_void_p()
-        rc = self._hip.hipHostMalloc(ctypes.byref(self._p), ctypes.c_size_t(max(int(nbytes), 1)), ctypes.c_uint(0))
-        if rc != 0 or not self._p.value:
-            raise RuntimeError(f"hipHostMalloc({nbytes}) failed: {rc}")
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(self._p.value))
+        _check(L.gasalx_host_alloc(ctypes.c_uint64(max(int(nbytes), 1)), ctypes.byref(self._p)), "host_alloc")
+        self.nbytes = int(nbytes)
+        self._finalizer = weakref.finalize(self, L.gasalx_host_free, ctypes.c_void_p(self._p.value))
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._p.value))
+        arr = raw[:self.nbytes].view(_PinnedArray)
+        arr._owner = self
+        self.array = arr
 
     def close(self):
-        if self._p is not None and self._p.value:
-            self.array = None
-            self._hip.hipHostFree(self._p)
-        self._p = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        self.array = None
 
 
 class Engine:

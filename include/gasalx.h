@@ -113,6 +113,12 @@ int gasalx_align_device(gasalx_engine *eng, const gasalx_params *params, const g
 int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gasalx_batch *host_batch,
                       const gasalx_results *host_out);
 
+/* Page-locked host memory from the HIP runtime libgasal itself uses (hipHostMalloc),
+ * for caller-owned input / result buffers (the reference's host pages and host_res
+ * are pinned: host_batch.cpp:79-153, res.cpp:8-70).  Freed with gasalx_host_free. */
+int gasalx_host_alloc(uint64_t bytes, void **out);
+int gasalx_host_free(void *ptr);
+
 /* Which kernel family the dispatcher selects for a batch (for tests/profiling):
  * writes a short NUL-terminated name into buf. */
 int gasalx_describe_plan(const gasalx_params *params, uint32_t max_q_len, uint32_t max_t_len, char *buf,

@@ -128,3 +128,24 @@ def test_batch_slice_matches_subset():
         if x.n:
             assert np.array_equal(x.q_data, y.q_data) and np.array_equal(x.t_offsets, y.t_offsets)
             assert np.array_equal(x.q_lens, y.q_lens)
+
+
+def test_pinned_host_lifetime_follows_its_arrays():
+    # gasalx_host_alloc is exported; without a device it fails loudly, with one the
+    # memory lives as long as any view (tests/test_gpu_parity.py covers the GPU side)
+    import gc
+    import weakref
+    try:
+        h = G.PinnedHost(64)
+    except RuntimeError:
+        pytest.skip("no HIP device for page-locked memory")
+    view = h.array[8:16]
+    ref = weakref.ref(h)
+    h.close()
+    del h
+    gc.collect()
+    assert ref() is not None          # the view still holds the owner
+    view[:] = 7
+    del view
+    gc.collect()
+    assert ref() is None

@@ -558,6 +558,14 @@ def test_host_pipeline_pinned_cigar(engine):
     for f in ("score", "q_end", "t_end", "q_start", "t_start", "n_ops", "cigar"):
         assert np.array_equal(got[f], ref[f]), f
     host.close()
+    # the handle dropped before the call: the array alone keeps the pinned memory alive
+    import gc
+    arr = G.PinnedHost(batch.q_bytes).array
+    gc.collect()
+    got = engine.align_host(batch, gp, cigar_out=arr)
+    del arr
+    gc.collect()
+    assert np.array_equal(got["cigar"], ref["cigar"])
 
 
 @pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL])
