@@ -35,12 +35,14 @@ struct gasalx_engine {
     gx::DevBuf q, t, qo, to, ql, tl, qop, top, seed;
     gx::DevBuf o_score, o_qe, o_te, o_qs, o_ts, o_s2, o_qe2, o_te2, o_cig, o_nops, lens_max;
     gx::DevBuf h_reads, h_ro, h_rl, h_qm, h_de, h_xi, h_al, h_haps, h_ho, h_hl, h_res;
+    gx::DevBuf h_bq, h_iq, h_dq, h_perm, ph2pr;   // PairHMM from qualities: staging + the ph2pr table
     void release() {
         ws.release_all();
         for (HostSlot &s : slot) s.release();
         for (gx::DevBuf *b : {&q, &t, &qo, &to, &ql, &tl, &qop, &top, &seed, &o_score, &o_qe, &o_te, &o_qs, &o_ts,
                               &o_s2, &o_qe2, &o_te2, &o_cig, &o_nops, &lens_max, &h_reads, &h_ro, &h_rl, &h_qm,
-                              &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res})
+                              &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res, &h_bq, &h_iq, &h_dq, &h_perm,
+                              &ph2pr})
             b->release();
     }
 };
@@ -428,11 +430,105 @@ int gasalx_pairhmm_host(gasalx_engine *eng, const gasalx_hmm_batch *hb, float *h
     return GASALX_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// ph2pr[q] = powf(10, -q/10) on the host, as the reference builds it (tile_1.cu:216-220)
+void ph2pr_table(float *t) {
+    for (int i = 0; i < 128; i++) t[i] = powf(10.f, -((float)i) / 10.f);
+}
+
+// The engine's device copy of the table (uploaded once, synchronously).
+int ph2pr_device(gasalx_engine *eng, const float **out) {
+    if (!eng->ph2pr.p) {
+        float t[128];
+        ph2pr_table(t);
+        CK(eng->ph2pr.reserve(sizeof(t)));
+        CK(hipMemcpy(eng->ph2pr.p, t, sizeof(t), hipMemcpyHostToDevice));
+    }
+    *out = eng->ph2pr.as<float>();
+    return GASALX_OK;
+}
+
+bool hmm_qual_batch_ok(const gasalx_hmm_qual_batch *b) {
+    return b && (b->n_pairs == 0 || (b->reads && b->read_offsets && b->read_lens && b->base_quals && b->ins_quals &&
+                                     b->del_quals && b->haps && b->hap_offsets && b->hap_lens));
+}
+
+}  // namespace
+
+extern "C" {
+
+int gasalx_pairhmm_quals_device(gasalx_engine *eng, const gasalx_hmm_qual_batch *b, float *res, void *stream) {
+    if (!eng || !hmm_qual_batch_ok(b) || !res) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    uint32_t mr = b->max_read_len, mh = b->max_hap_len;
+    if ((!mr || !mh) && b->n_pairs) {
+        int rc = device_max_lens(eng, b->read_lens, b->hap_lens, b->n_pairs, st, &mr, &mh);
+        if (rc) return rc;
+    }
+    const float *tab;
+    int rc = ph2pr_device(eng, &tab);
+    if (rc) return rc;
+    return gx::pairhmm_quals_device(eng->ws, *b, res, st, tab, nullptr, nullptr, 0, mr, mh);
+}
+
+int gasalx_pairhmm_quals_host(gasalx_engine *eng, const gasalx_hmm_qual_batch *hb, float *hres) {
+    if (!eng || !hmm_qual_batch_ok(hb) || !hres) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    const uint32_t n = hb->n_pairs;
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    // slots in (read length, haplotype length) order (tile_1.cu:180-195 operator<, :325)
+    std::vector<uint32_t> perm(n);
+    for (uint32_t i = 0; i < n; i++) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](uint32_t x, uint32_t y) {
+        const uint32_t rx = hb->read_lens[x], ry = hb->read_lens[y];
+        return rx != ry ? rx < ry : hb->hap_lens[x] < hb->hap_lens[y];
+    });
+    // classes: runs of slots whose reads need the same lane-group size
+    std::vector<gx::HmmClass> classes;
+    for (uint32_t s = 0; s < n; s++) {
+        const uint32_t r = hb->read_lens[perm[s]], h = hb->hap_lens[perm[s]];
+        const int g = gx::pairhmm_group(r);
+        if (classes.empty() || gx::pairhmm_group(classes.back().max_r) != g) classes.push_back({s, s, 0, 0});
+        gx::HmmClass &c = classes.back();
+        c.slot1 = s + 1;
+        c.max_r = std::max(c.max_r, r);
+        c.max_h = std::max(c.max_h, h);
+    }
+    gasalx_hmm_qual_batch db = *hb;
+    int rc;
+    uint8_t *p8; uint32_t *p32;
+    if ((rc = stage_in(eng->h_reads, hb->reads, hb->read_bytes, st, &p8))) return rc; db.reads = p8;
+    if ((rc = stage_in(eng->h_bq, hb->base_quals, hb->read_bytes, st, &p8))) return rc; db.base_quals = p8;
+    if ((rc = stage_in(eng->h_iq, hb->ins_quals, hb->read_bytes, st, &p8))) return rc; db.ins_quals = p8;
+    if ((rc = stage_in(eng->h_dq, hb->del_quals, hb->read_bytes, st, &p8))) return rc; db.del_quals = p8;
+    if ((rc = stage_in(eng->h_ro, hb->read_offsets, n, st, &p32))) return rc; db.read_offsets = p32;
+    if ((rc = stage_in(eng->h_rl, hb->read_lens, n, st, &p32))) return rc; db.read_lens = p32;
+    if ((rc = stage_in(eng->h_haps, hb->haps, hb->hap_bytes, st, &p8))) return rc; db.haps = p8;
+    if ((rc = stage_in(eng->h_ho, hb->hap_offsets, n, st, &p32))) return rc; db.hap_offsets = p32;
+    if ((rc = stage_in(eng->h_hl, hb->hap_lens, n, st, &p32))) return rc; db.hap_lens = p32;
+    uint32_t *dperm;
+    if ((rc = stage_in(eng->h_perm, perm.data(), n, st, &dperm))) return rc;
+    CK(eng->h_res.reserve((size_t)n * 4 + 16));
+    const float *tab;
+    if ((rc = ph2pr_device(eng, &tab))) return rc;
+    rc = gx::pairhmm_quals_device(eng->ws, db, eng->h_res.as<float>(), st, tab, dperm, classes.data(),
+                                  (int)classes.size(), 0, 0);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    CK(hipMemcpyAsync(hres, eng->h_res.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
 int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *dq, uint32_t n, float *qm,
                           float *delta, float *xiksi, float *alpha) {
     if (n && (!bq || !iq || !dq || !qm || !delta || !xiksi || !alpha)) return GASALX_EINVAL;
     float ph2pr[128];
-    for (int i = 0; i < 128; i++) ph2pr[i] = powf(10.f, -((float)i) / 10.f);   // tile_1.cu:216-220
+    ph2pr_table(ph2pr);
     for (uint32_t k = 0; k < n; k++) {                                         // :415-419
         qm[k] = ph2pr[bq[k] & 127];
         delta[k] = ph2pr[iq[k] & 127];

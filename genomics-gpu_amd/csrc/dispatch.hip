@@ -538,7 +538,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                 }
                 gen_semi_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
             } else if (p.algo == 5) gen_banded_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
-            else { set_error("global lengths beyond the wavefront shapes are not supported"); return GASALX_ERANGE; }
+            else gen_global_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
         }
         HIPCHK(hipGetLastError());
     }
@@ -585,38 +585,73 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
 
 // ----------------------------------------------------------------------------
 using HmmFn = void (*)(HmmArgs);
-static HmmFn hmm_lookup(int G, int RR) {
-    if (RR != 8) return nullptr;
+template <bool QUALS>
+static HmmFn hmm_lookup(int G) {
     switch (G) {
-        case 4: return &pairhmm_kernel<4, 8>;
-        case 8: return &pairhmm_kernel<8, 8>;
-        case 16: return &pairhmm_kernel<16, 8>;
-        case 32: return &pairhmm_kernel<32, 8>;
-        case 64: return &pairhmm_kernel<64, 8>;
+        case 4: return &pairhmm_kernel<4, 8, QUALS>;
+        case 8: return &pairhmm_kernel<8, 8, QUALS>;
+        case 16: return &pairhmm_kernel<16, 8, QUALS>;
+        case 32: return &pairhmm_kernel<32, 8, QUALS>;
+        case 64: return &pairhmm_kernel<64, 8, QUALS>;
         default: return nullptr;
     }
+}
+
+// lanes per pair for a read of max_r rows: 8 rows per lane, G in {4, ..., 64}
+int pairhmm_group(uint32_t max_r) {
+    for (int g : {4, 8, 16, 32, 64})
+        if ((uint32_t)g * 8 >= max_r) return g;
+    return 0;
+}
+
+// One launch over slots [slot0, slot1) of A (A.perm maps slots to pairs, or NULL).
+static int pairhmm_launch(HmmArgs A, bool quals, int G, uint32_t slot0, uint32_t slot1, uint32_t max_h,
+                          hipStream_t st) {
+    if (slot1 <= slot0) return GASALX_OK;
+    if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
+    A.slot0 = slot0;
+    A.n = slot1;
+    A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
+    const size_t lds = (size_t)4 * (64 / G) * A.lds_stride;
+    if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
+    HmmFn fn = quals ? hmm_lookup<true>(G) : hmm_lookup<false>(G);
+    if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);
+    HIPCHK(hipGetLastError());
+    return GASALX_OK;
 }
 
 int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipStream_t st, uint32_t max_r,
                    uint32_t max_h) {
     (void)ws;
     if (b.n_pairs == 0) return GASALX_OK;
-    int G = 0;
-    for (int g : {4, 8, 16, 32, 64})
-        if ((uint32_t)g * 8 >= max_r) { G = g; break; }
-    if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
     HmmArgs A;
+    std::memset(&A, 0, sizeof(A));
     A.reads = b.reads; A.roff = b.read_offsets; A.rlen = b.read_lens;
     A.qm = b.qm; A.delta = b.delta; A.xiksi = b.xiksi; A.alpha = b.alpha;
     A.haps = b.haps; A.hoff = b.hap_offsets; A.hlen = b.hap_lens;
-    A.result = result; A.n = b.n_pairs;
-    A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
-    const size_t lds = (size_t)4 * (64 / G) * A.lds_stride;
-    if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
-    HmmFn fn = hmm_lookup(G, 8);
-    if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(fn, dim3(grid_for(b.n_pairs, 4 * (64 / G))), dim3(256), lds, st, A);
-    HIPCHK(hipGetLastError());
+    A.result = result;
+    return pairhmm_launch(A, false, pairhmm_group(max_r), 0, b.n_pairs, max_h, st);
+}
+
+int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *result, hipStream_t st,
+                         const float *ph2pr_dev, const uint32_t *perm, const HmmClass *classes, int n_classes,
+                         uint32_t max_r, uint32_t max_h) {
+    (void)ws;
+    if (b.n_pairs == 0) return GASALX_OK;
+    HmmArgs A;
+    std::memset(&A, 0, sizeof(A));
+    A.reads = b.reads; A.roff = b.read_offsets; A.rlen = b.read_lens;
+    A.bq = b.base_quals; A.iq = b.ins_quals; A.dq = b.del_quals; A.ph2pr = ph2pr_dev;
+    A.haps = b.haps; A.hoff = b.hap_offsets; A.hlen = b.hap_lens;
+    A.result = result;
+    A.perm = perm;
+    if (!classes) return pairhmm_launch(A, true, pairhmm_group(max_r), 0, b.n_pairs, max_h, st);
+    for (int c = 0; c < n_classes; c++) {
+        int rc = pairhmm_launch(A, true, pairhmm_group(classes[c].max_r), classes[c].slot0, classes[c].slot1,
+                                classes[c].max_h, st);
+        if (rc) return rc;
+    }
     return GASALX_OK;
 }
 

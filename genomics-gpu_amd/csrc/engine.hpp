@@ -88,6 +88,15 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
 int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipStream_t stream, uint32_t max_r,
                    uint32_t max_h);
 
+// PairHMM from Phred qualities.  ph2pr_dev: the 128-entry table in device memory.
+// With perm/classes (host path): slots sorted by (read, haplotype) length, one launch
+// per class of slots sharing a lane-group size; otherwise one launch over all pairs.
+struct HmmClass { uint32_t slot0, slot1, max_r, max_h; };
+int pairhmm_group(uint32_t max_r);
+int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *result, hipStream_t stream,
+                         const float *ph2pr_dev, const uint32_t *perm, const HmmClass *classes, int n_classes,
+                         uint32_t max_r, uint32_t max_h);
+
 void set_error(const std::string &msg);
 const char *last_error();
 

@@ -146,6 +146,79 @@ __global__ __launch_bounds__(256) void gen_local_kernel(GenArgs A) {
 #undef RE
 }
 
+// --------------------------------------------------------------- global ----
+// GLOBAL beyond the wavefront shapes (padded query > 1280, or values outside
+// the range where int32 arithmetic without the int16 row buffer is exact):
+// kernels/global.h:30-303.  Left column H(r, -1) = -(o + e*r) with H(0, -1) = 0
+// (Q2), top row only through the diagonal, F = -inf at every strip start, no
+// N rule (GLOBAL macro), (H, E) carried between strips as int16 (Q5), score =
+// H(ql-1, tl-1) captured on the row ql-1 of the last strip (:98-103, :299).
+__global__ __launch_bounds__(256) void gen_global_kernel(GenArgs A) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= A.n) return;
+    const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
+    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
+    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
+    const uint32_t QR = (ql + 7) >> 3, TR = (tl + 7) >> 3, Q8 = QR * 8;
+    const bool tb = A.start_pos == 2;
+    const int32_t OE = A.o + A.e;
+    auto sub = [&](uint32_t q, uint32_t t) {   // DEV_GET_SUB_SCORE_GLOBAL (gasal_kernels.h:44-54)
+        int32_t v = (q == t) ? A.a : -A.b;
+        if (A.has_npen && ((int32_t)q == A.nval || (int32_t)t == A.nval)) v = -A.npen;
+        return v;
+    };
+#define RH(r) A.rowH[(size_t)(r) * A.n + tid]
+#define RE(r) A.rowE[(size_t)(r) * A.n + tid]
+    for (uint32_t r = 0; r < Q8; r++) {
+        RH(r) = (int16_t)(r == 0 ? 0 : -(A.o + A.e * (int32_t)r));
+        RE(r) = (int16_t)-32768;
+    }
+    int32_t h[9], f[9], p[9], last[9];
+    for (int m = 0; m < 9; m++) last[m] = 0;
+    h[0] = 0; p[0] = 0;
+    for (uint32_t i = 0; i < TR; i++) {
+        const int32_t c0 = (int32_t)(i << 3);
+        for (int m = 1; m < 9; m++) {                       // :67-71 (u = column + 1, r = column)
+            const int32_t col = c0 + m - 1;
+            h[m] = -(A.o + A.e * (col + 1));
+            f[m] = -32768;
+            p[m] = col == 0 ? 0 : -(A.o + A.e * col);
+        }
+        const uint32_t gpac = tw[i];
+        for (uint32_t r = 0; r < Q8; r++) {
+            const uint32_t qb = gcode(qw, r);
+            uint32_t dword = 0;
+            h[0] = RH(r);
+            int32_t e = RE(r);
+#pragma unroll
+            for (int m = 1; m <= 8; m++) {
+                const uint32_t tbase = (gpac >> (28 - 4 * (m - 1))) & 15u;
+                const int32_t tmp = p[m] + sub(qb, tbase);
+                const int32_t H = max(max(tmp, f[m]), e);
+                if (tb) {                                   // CORE_GLOBAL_COMPUTE_TB (:14-26)
+                    const int sh = 28 - ((m - 1) << 2);
+                    const uint32_t mxo = (tmp >= p[m]) ? 0u : 1u;
+                    dword |= (H == tmp) ? (mxo << sh) : ((H == f[m]) ? (3u << sh) : (2u << sh));
+                    dword |= ((tmp - OE) > (f[m] - A.e)) ? 0u : (1u << (sh + 3));
+                    dword |= ((tmp - OE) > (e - A.e)) ? 0u : (1u << (sh + 2));
+                }
+                f[m] = max(tmp - OE, f[m] - A.e);
+                e = max(tmp - OE, e - A.e);
+                h[m] = H;
+                p[m] = h[m - 1];
+            }
+            RH(r) = (int16_t)h[8];
+            RE(r) = (int16_t)e;
+            if (tb) A.tb[(uint64_t)tid * A.tb_pair_words + (uint64_t)i * Q8 + r] = dword;
+            if (r + 1 == ql)
+                for (int m = 1; m < 9; m++) last[m] = h[m];
+        }
+    }
+    A.score[tid] = last[8 - ((TR << 3) - tl)];
+#undef RH
+#undef RE
+}
+
 // ----------------------------------------------------------- semi-global ----
 __device__ __forceinline__ void semi_rows_init(const GenArgs &A, uint32_t tid, uint32_t nrow) {
     const bool hq = (A.head == 1 || A.head == 3);

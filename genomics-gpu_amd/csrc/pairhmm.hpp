@@ -22,22 +22,31 @@ struct HmmArgs {
     float *result;
     uint32_t n;
     uint32_t lds_stride;   // bytes per pair slot (>= max haplotype length, multiple of 4)
+    // QUALS kernels: Phred qualities per read base (at the read offsets) instead of
+    // the four float parameters, mapped through the host's ph2pr table exactly as the
+    // reference's host code does (tile_1.cu:216-220 table, :415-419 mapping)
+    const uint8_t *bq, *iq, *dq;
+    const float *ph2pr;    // 128 entries
+    // length classes (dispatch.hip): this launch covers slots [slot0, n); slot -> pair
+    // through perm (pairs sorted by read then haplotype length, tile_1.cu:180-195,325)
+    const uint32_t *perm;
+    uint32_t slot0;
 };
 
 __device__ __forceinline__ float shr_lane_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
 }
 
-template <int G, int RR>
+template <int G, int RR, bool QUALS = false>
 __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int P = 64 / G;
     const float c0 = 1.329228e+36f, c09 = 0.9f, c01 = 0.1f;     // tile_1.cu:228-233
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1), slot = lane / G;
-    const uint32_t pair0 = (blockIdx.x * 4 + wave) * P;
-    const uint32_t pair = pair0 + slot;
-    const bool valid = pair < A.n;
+    const uint32_t idx = A.slot0 + (blockIdx.x * 4 + wave) * P + slot;
+    const bool valid = idx < A.n;
+    const uint32_t pair = (valid && A.perm) ? A.perm[idx] : idx;
     uint32_t R = 0, H = 0, ro = 0, ho = 0;
     if (valid) { R = A.rlen[pair]; H = A.hlen[pair]; ro = A.roff[pair]; ho = A.hoff[pair]; }
 
@@ -74,13 +83,24 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     for (int k = 0; k < RR; ++k) {
         const int32_t i = r0 + k;
         const bool in = valid && i >= 0;
-        const float q = in ? A.qm[ro + i] : 0.f;
+        float q = 0.f, d = 0.f, x = 0.f, a = 0.f;
+        if (in) {
+            if (QUALS) {
+                const uint32_t b = A.bq[ro + i] & 127u, iqv = A.iq[ro + i] & 127u, dqv = A.dq[ro + i] & 127u;
+                q = A.ph2pr[b];
+                d = A.ph2pr[iqv];
+                x = A.ph2pr[dqv];
+                a = __fsub_rn(1.0f, A.ph2pr[(iqv + dqv) & 127u]);
+            } else {
+                q = A.qm[ro + i]; d = A.delta[ro + i]; x = A.xiksi[ro + i]; a = A.alpha[ro + i];
+            }
+        }
         rb[k] = in ? A.reads[ro + i] : 0x100u;
         qm1[k] = in ? __fsub_rn(1.0f, q) : 0.f;     // Qm_1 = constant[1] - Qm
         qm3[k] = in ? __fdiv_rn(q, 3.0f) : 0.f;     // fdividef(Qm, 3) (<= 2 ulp in the reference)
-        de[k] = in ? A.delta[ro + i] : 0.f;
-        xi[k] = in ? A.xiksi[ro + i] : 0.f;
-        al[k] = in ? A.alpha[ro + i] : 0.f;
+        de[k] = d;
+        xi[k] = x;
+        al[k] = a;
         dk[k] = in ? c01 : 1.0f;
         Mk[k] = 0.f;
         Dk[k] = in ? 0.f : D0;

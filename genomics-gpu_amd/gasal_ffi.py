@@ -31,6 +31,7 @@ EXPORTS = (
     "gasalx_engine_destroy", "gasalx_align_device", "gasalx_align_host", "gasalx_describe_plan",
     "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
     "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
+    "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
 )
 
 
@@ -60,6 +61,22 @@ class CHmmBatch(ctypes.Structure):
                 ("alpha", ctypes.c_void_p), ("haps", ctypes.c_void_p), ("hap_offsets", ctypes.c_void_p),
                 ("hap_lens", ctypes.c_void_p), ("read_bytes", ctypes.c_uint32), ("hap_bytes", ctypes.c_uint32),
                 ("n_pairs", ctypes.c_uint32), ("max_read_len", ctypes.c_uint32), ("max_hap_len", ctypes.c_uint32)]
+
+
+class CHmmQualBatch(ctypes.Structure):
+    _fields_ = [("reads", ctypes.c_void_p), ("read_offsets", ctypes.c_void_p), ("read_lens", ctypes.c_void_p),
+                ("base_quals", ctypes.c_void_p), ("ins_quals", ctypes.c_void_p), ("del_quals", ctypes.c_void_p),
+                ("haps", ctypes.c_void_p), ("hap_offsets", ctypes.c_void_p), ("hap_lens", ctypes.c_void_p),
+                ("read_bytes", ctypes.c_uint64), ("hap_bytes", ctypes.c_uint64), ("n_pairs", ctypes.c_uint32),
+                ("max_read_len", ctypes.c_uint32), ("max_hap_len", ctypes.c_uint32)]
+
+
+class CHmmFile(ctypes.Structure):
+    _fields_ = [("n_pairs", ctypes.c_uint32), ("n_groups", ctypes.c_uint32), ("group_sizes", ctypes.c_void_p),
+                ("reads", ctypes.c_void_p), ("read_offsets", ctypes.c_void_p), ("read_lens", ctypes.c_void_p),
+                ("base_quals", ctypes.c_void_p), ("ins_quals", ctypes.c_void_p), ("del_quals", ctypes.c_void_p),
+                ("gcp_quals", ctypes.c_void_p), ("haps", ctypes.c_void_p), ("hap_offsets", ctypes.c_void_p),
+                ("hap_lens", ctypes.c_void_p), ("read_bytes", ctypes.c_uint64), ("hap_bytes", ctypes.c_uint64)]
 
 
 _lib = None
@@ -282,6 +299,14 @@ class Engine:
         _check(lib().gasalx_pairhmm_host(self._h, ctypes.byref(hb), _p(res)), "pairhmm_host")
         return res
 
+    def pairhmm_quals_host(self, hmm: "HmmData"):
+        """PairHMM from Phred qualities (the reference's input files): sorted by length,
+        one launch per lane-group class; results in input order."""
+        res = np.zeros(hmm.n, np.float32)
+        hb = hmm.cstruct()
+        _check(lib().gasalx_pairhmm_quals_host(self._h, ctypes.byref(hb), _p(res)), "pairhmm_quals_host")
+        return res
+
     def pairhmm_device_ptrs(self, ptrs: dict, read_bytes: int, hap_bytes: int, n: int, max_r: int, max_h: int,
                             result_ptr: int, stream: int = 0):
         g = lambda k: ptrs.get(k) or None
@@ -302,6 +327,71 @@ def describe_plan(params: Params, max_q: int, max_t: int) -> str:
     buf = ctypes.create_string_buffer(128)
     _check(lib().gasalx_describe_plan(ctypes.byref(params), max_q, max_t, buf, 128), "describe_plan")
     return buf.value.decode()
+
+
+@dataclass
+class HmmData:
+    """PairHMM pairs in the reference's input terms: reads with base / insertion /
+    deletion / gcp qualities and haplotypes (tile_1.cu:246-290)."""
+    reads: np.ndarray
+    read_offsets: np.ndarray
+    read_lens: np.ndarray
+    base_quals: np.ndarray
+    ins_quals: np.ndarray
+    del_quals: np.ndarray
+    gcp_quals: np.ndarray
+    haps: np.ndarray
+    hap_offsets: np.ndarray
+    hap_lens: np.ndarray
+    group_sizes: np.ndarray
+
+    @property
+    def n(self):
+        return len(self.read_lens)
+
+    def cstruct(self) -> CHmmQualBatch:
+        return CHmmQualBatch(_p(self.reads), _p(self.read_offsets), _p(self.read_lens), _p(self.base_quals),
+                             _p(self.ins_quals), _p(self.del_quals), _p(self.haps), _p(self.hap_offsets),
+                             _p(self.hap_lens), len(self.reads), len(self.haps), self.n,
+                             int(self.read_lens.max(initial=0)), int(self.hap_lens.max(initial=0)))
+
+    @classmethod
+    def from_pairs(cls, pairs):
+        """pairs: dicts with read, hap (str/bytes) and bq, iq, dq (, gcp) sequences."""
+        enc = lambda s: s.encode() if isinstance(s, str) else bytes(s)
+        reads = [enc(p["read"]) for p in pairs]
+        haps = [enc(p["hap"]) for p in pairs]
+        rl = np.array([len(r) for r in reads], np.uint32)
+        hl = np.array([len(h) for h in haps], np.uint32)
+        ro = np.concatenate([[0], np.cumsum(rl, dtype=np.uint64)[:-1]]).astype(np.uint32)
+        ho = np.concatenate([[0], np.cumsum(hl, dtype=np.uint64)[:-1]]).astype(np.uint32)
+        q = lambda k: np.concatenate([np.asarray(p.get(k, np.zeros(len(p["read"]))), np.int64)
+                                      for p in pairs]).astype(np.uint8)
+        return cls(np.frombuffer(b"".join(reads), np.uint8).copy(), ro, rl, q("bq"), q("iq"), q("dq"), q("gcp"),
+                   np.frombuffer(b"".join(haps), np.uint8).copy(), ho, hl, np.array([len(pairs)], np.uint32))
+
+    def float_params(self):
+        """The reference host's four per-base parameters (tile_1.cu:415-419)."""
+        return pairhmm_params(self.base_quals, self.ins_quals, self.del_quals)
+
+
+def read_hmm_file(path: str) -> HmmData:
+    """Parse a reference PairHMM input file with the library's native reader
+    (gasalx_hmm_file_read)."""
+    h = ctypes.POINTER(CHmmFile)()
+    _check(lib().gasalx_hmm_file_read(os.fsencode(path), ctypes.byref(h)), "hmm_file_read")
+    try:
+        f = h.contents
+        n, rb, hb = f.n_pairs, f.read_bytes, f.hap_bytes
+        arr = lambda ptr, cnt, t: np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(t)), (cnt,)).copy() \
+            if cnt else np.zeros(0, np.dtype(t))
+        u8, u32 = ctypes.c_uint8, ctypes.c_uint32
+        return HmmData(arr(f.reads, rb, u8), arr(f.read_offsets, n, u32), arr(f.read_lens, n, u32),
+                       arr(f.base_quals, rb, u8), arr(f.ins_quals, rb, u8), arr(f.del_quals, rb, u8),
+                       arr(f.gcp_quals, rb, u8), arr(f.haps, hb, u8), arr(f.hap_offsets, n, u32),
+                       arr(f.hap_lens, n, u32), arr(f.group_sizes, f.n_groups, u32))
+    finally:
+        lib().gasalx_hmm_file_free(h)
 
 
 def pairhmm_params(bq, iq, dq):

@@ -153,6 +153,61 @@ int gasalx_pairhmm_host(gasalx_engine *eng, const gasalx_hmm_batch *host_batch, 
 int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *dq, uint32_t n, float *qm,
                           float *delta, float *xiksi, float *alpha);
 
+/* PairHMM from Phred qualities: the reference's input format (tile_1.cu:246-290,
+ * Intra-task/real_data/improved_warp_based/improved_warp_based.cu:240-279).  base /
+ * insertion / deletion quality bytes sit at the read offsets; the four per-base
+ * parameters are formed on the device from the same ph2pr table the reference's host
+ * builds (powf(10, -q/10), tile_1.cu:216-220; mapping :415-419), so the kernel's
+ * input is 4 bytes per read base instead of 17. */
+typedef struct gasalx_hmm_qual_batch {
+    const uint8_t *reads;
+    const uint32_t *read_offsets;
+    const uint32_t *read_lens;
+    const uint8_t *base_quals;
+    const uint8_t *ins_quals;
+    const uint8_t *del_quals;
+    const uint8_t *haps;
+    const uint32_t *hap_offsets;
+    const uint32_t *hap_lens;
+    uint64_t read_bytes;          /* bytes of reads (and of each quality array) */
+    uint64_t hap_bytes;
+    uint32_t n_pairs;
+    uint32_t max_read_len;        /* upper bounds (0 = unknown) */
+    uint32_t max_hap_len;
+} gasalx_hmm_qual_batch;
+
+/* Device-resident batch: one launch, lane groups sized by the longest read. */
+int gasalx_pairhmm_quals_device(gasalx_engine *eng, const gasalx_hmm_qual_batch *dev_batch, float *dev_result,
+                                void *stream);
+/* Host arrays in, results out in input order.  Pairs run sorted by (read length,
+ * haplotype length) as the reference's host sorts them (tile_1.cu:180-195,325), in
+ * classes of reads that share a lane-group size (one launch each) instead of the
+ * reference's 32-pair interleaved chunks (tile_1.cu:346-500). */
+int gasalx_pairhmm_quals_host(gasalx_engine *eng, const gasalx_hmm_qual_batch *host_batch, float *host_result);
+
+/* Reader of the reference's PairHMM input files: groups of `size` pairs, each pair
+ * = read length, read bases, then read-length base / insertion / deletion / gcp
+ * qualities, haplotype length, haplotype bases (whitespace-separated, fscanf
+ * semantics of tile_1.cu:246-290; qualities stored as (char) values).  Arrays are
+ * owned by the returned object (gasalx_hmm_file_free). */
+typedef struct gasalx_hmm_file {
+    uint32_t n_pairs;
+    uint32_t n_groups;
+    uint32_t *group_sizes;        /* pairs per group, in file order */
+    uint8_t *reads;
+    uint32_t *read_offsets;
+    uint32_t *read_lens;
+    uint8_t *base_quals, *ins_quals, *del_quals, *gcp_quals;
+    uint8_t *haps;
+    uint32_t *hap_offsets;
+    uint32_t *hap_lens;
+    uint64_t read_bytes;
+    uint64_t hap_bytes;
+} gasalx_hmm_file;
+
+int gasalx_hmm_file_read(const char *path, gasalx_hmm_file **out);
+int gasalx_hmm_file_free(gasalx_hmm_file *f);
+
 /* Synthetic workloads of SURVEY.md §8(d) (benchmark/test data, std::mt19937_64).
  * Writes a GASAL2-layout batch (N_CODE padding) into caller buffers sized by
  * gasalx_synth_sizes.  kind: 1..4 = configs 1..4.  Pairs come in blocks of 65,536,

@@ -216,6 +216,25 @@ def test_global_random(engine, qr, tr):
     check(engine, b, algo=G.GLOBAL)
 
 
+@pytest.mark.parametrize("qr,tr,tb", [((1490, 1500), (1490, 1500), False), ((1490, 1500), (1490, 1500), True),
+                                      ((990, 1000), (1990, 2000), False), ((990, 1000), (1990, 2000), True)])
+def test_global_long_reads_thread_per_pair(engine, qr, tr, tb):
+    # beyond the wavefront shapes (padded query > 1280) or the exact-int32 range
+    # (q + t above ~2.7 kb at 1/4/6/1): the thread-per-pair kernel with the
+    # reference's int16 row buffer (global.h:30-303), with and without traceback
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB if tb else G.WITHOUT_START)
+    assert G.describe_plan(G.make_params(**kw), qr[1], tr[1]) == "generic_global"
+    b = rand_batch(0x610B + qr[0] + tb, 48, *qr, *tr, related=0.8)
+    check(engine, no_cigar_overflow(b, **kw) if tb else b, cigar=tb, **kw)
+
+
+def test_global_int16_row_buffer_wrap(engine):
+    # large scores over 3 kb: row-buffer values leave int16 and wrap as in the reference (Q5)
+    kw = dict(algo=G.GLOBAL, match=9, mismatch=12, gap_open=20, gap_extend=5)
+    assert G.describe_plan(G.make_params(**kw), 3000, 3000) == "generic_global"
+    check(engine, rand_batch(0x610C, 16, 2900, 3000, 2900, 3000, related=0.9), **kw)
+
+
 def test_global_traceback_len_not_mult8(engine):
     rng = np.random.default_rng(32)
     qs, ts = [], []
@@ -686,3 +705,69 @@ def test_gpu_against_independent_restatement(engine, head, tail):
         assert np.array_equal(g[f], r[f]), f
     g = engine.align_host(b, G.make_params(algo=G.GLOBAL))
     assert np.array_equal(g["score"], I.global_(b)["score"])
+
+
+# ------------------------------------- PairHMM from qualities (input files) ----
+def _hmm_oracle(d):
+    qm, de, xi, al = O.pairhmm_params(d.base_quals, d.ins_quals, d.del_quals)
+    return O.pairhmm(d.reads, d.read_offsets, d.read_lens, qm, de, xi, al, d.haps, d.hap_offsets, d.hap_lens)
+
+
+def _hmm_float(engine, d):
+    qm, de, xi, al = d.float_params()
+    return engine.pairhmm_host(d.reads, d.read_offsets, d.read_lens, qm, de, xi, al, d.haps, d.hap_offsets,
+                               d.hap_lens)
+
+
+def test_pairhmm_quals_reference_files(engine):
+    # every reference dataset file (Intra-task and inter_task synthetic sets) through the
+    # native reader and the quality-input kernels; == the float-parameter path bit for bit
+    import glob
+    files = sorted(glob.glob(os.path.join(helpers.GOLDEN, "pairhmm_dataset", "*.txt")) +
+                   glob.glob(os.path.join(helpers.GOLDEN, "pairhmm_inter_dataset", "*.txt")))
+    for f in files:
+        d = G.read_hmm_file(f)
+        g = engine.pairhmm_quals_host(d)
+        np.testing.assert_allclose(g, _hmm_oracle(d), rtol=1e-5, err_msg=f)
+        assert np.array_equal(g.view(np.uint32), _hmm_float(engine, d).view(np.uint32)), f
+
+
+def test_pairhmm_quals_sorted_classes_mixed_lengths(engine):
+    # reads of 1..512 bases (all five lane-group classes) and haplotypes of 1..700 in
+    # random order: sorted by length on the host (tile_1.cu:325), one launch per class,
+    # results back in input order
+    rng = np.random.default_rng(0x4D32)
+    pairs = []
+    for _ in range(3000):
+        R = int(rng.integers(1, 513))
+        H = int(rng.integers(1, 701))
+        hap = helpers.random_seq(rng, H).decode()
+        read = helpers.random_seq(rng, R).decode() if rng.random() < 0.3 else (hap * (R // H + 1))[:R]
+        pairs.append(dict(read=read, hap=hap, bq=rng.integers(0, 256, R), iq=rng.integers(0, 128, R),
+                          dq=rng.integers(0, 128, R)))
+    d = G.HmmData.from_pairs(pairs)
+    g = engine.pairhmm_quals_host(d)
+    np.testing.assert_allclose(g, _hmm_oracle(d), rtol=1e-5)
+    assert np.array_equal(g.view(np.uint32), _hmm_float(engine, d).view(np.uint32))
+
+
+def test_pairhmm_prog_driver(tmp_path):
+    # the driver binary (tools/pairhmm_prog, C-ABI client): a multi-group file, every
+    # result line against the oracle; -fakesize replicates pair 0 as the reference does
+    import subprocess
+    from test_hmm_io import _rand_pairs, _write_groups
+    rng = np.random.default_rng(0x4D33)
+    groups = [_rand_pairs(rng, 40), _rand_pairs(rng, 7)]
+    path = tmp_path / "in.txt"
+    _write_groups(path, groups)
+    prog = os.path.join(os.path.dirname(helpers.GOLDEN), "..", "tools", "pairhmm_prog")
+    out = subprocess.run([prog, "-print", "all", str(path)], capture_output=True, text=True, check=True).stdout
+    vals = [float(l.split()[1]) for l in out.splitlines() if l.startswith("  i=")]
+    d = G.read_hmm_file(str(path))
+    np.testing.assert_allclose(np.array(vals, np.float32), _hmm_oracle(d), rtol=1e-5)
+    assert "GCUPS:" in out
+    out = subprocess.run([prog, "-fakesize", "1000", "-print", "last", str(path)], capture_output=True, text=True,
+                         check=True).stdout
+    lines = [l for l in out.splitlines() if l.startswith("  i=")]
+    assert len(lines) == 2 and lines[0].startswith("  i=999")
+    np.testing.assert_allclose(float(lines[0].split()[1]), _hmm_oracle(d)[0], rtol=1e-5)
