@@ -36,13 +36,14 @@ struct gasalx_engine {
     gx::DevBuf o_score, o_qe, o_te, o_qs, o_ts, o_s2, o_qe2, o_te2, o_cig, o_nops, lens_max;
     gx::DevBuf h_reads, h_ro, h_rl, h_qm, h_de, h_xi, h_al, h_haps, h_ho, h_hl, h_res;
     gx::DevBuf h_bq, h_iq, h_dq, h_perm, ph2pr;   // PairHMM from qualities: staging + the ph2pr table
+    gx::DevBuf nv_pw, nv_po, nv_tw, nv_to, nv_s, nv_s16;   // nvbio front-end staging
     void release() {
         ws.release_all();
         for (HostSlot &s : slot) s.release();
         for (gx::DevBuf *b : {&q, &t, &qo, &to, &ql, &tl, &qop, &top, &seed, &o_score, &o_qe, &o_te, &o_qs, &o_ts,
                               &o_s2, &o_qe2, &o_te2, &o_cig, &o_nops, &lens_max, &h_reads, &h_ro, &h_rl, &h_qm,
                               &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res, &h_bq, &h_iq, &h_dq, &h_perm,
-                              &ph2pr})
+                              &ph2pr, &nv_pw, &nv_po, &nv_tw, &nv_to, &nv_s, &nv_s16})
             b->release();
     }
 };
@@ -520,6 +521,64 @@ int gasalx_pairhmm_quals_host(gasalx_engine *eng, const gasalx_hmm_qual_batch *h
                                   (int)classes.size(), 0, 0);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(hres, eng->h_res.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
+namespace {
+// max over i of off[i+1] - off[i]
+uint32_t max_span(const uint32_t *off, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) m = std::max(m, off[i + 1] - off[i]);
+    return m;
+}
+}  // namespace
+
+int gasalx_nv_score_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t n, const gasalx_nv_strings *pat,
+                           const gasalx_nv_strings *txt, int32_t *scores, int16_t *scores16, uint32_t max_p,
+                           uint32_t max_t, void *stream) {
+    if (!eng || !al || !pat || !txt) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    if (n && (!max_p || (txt->offsets && !max_t))) {   // read the offsets back (synchronises the stream)
+        std::vector<uint32_t> po(n + 1), to(txt->offsets ? n + 1 : 0);
+        CK(hipMemcpyAsync(po.data(), pat->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        if (txt->offsets) CK(hipMemcpyAsync(to.data(), txt->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        if (!max_p) max_p = max_span(po.data(), n);
+        if (txt->offsets && !max_t) max_t = max_span(to.data(), n);
+    }
+    return gx::nv_score_device(*al, n, *pat, *txt, scores, scores16, max_p, max_t, st);
+}
+
+int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t n, const gasalx_nv_strings *pat,
+                         uint64_t pat_words, const gasalx_nv_strings *txt, uint64_t txt_words, int32_t *scores,
+                         int16_t *scores16) {
+    if (!eng || !al || !pat || !txt || !pat->words || !pat->offsets || !txt->words || (!scores && !scores16)) {
+        gx::set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    const uint32_t max_p = max_span(pat->offsets, n);
+    const uint32_t max_t = txt->offsets ? max_span(txt->offsets, n) : txt->length;
+    gasalx_nv_strings dp = *pat, dt = *txt;
+    int rc;
+    uint32_t *p32;
+    if ((rc = stage_in(eng->nv_pw, pat->words, pat_words, st, &p32))) return rc; dp.words = p32;
+    if ((rc = stage_in(eng->nv_po, pat->offsets, (size_t)n + 1, st, &p32))) return rc; dp.offsets = p32;
+    if ((rc = stage_in(eng->nv_tw, txt->words, txt_words, st, &p32))) return rc; dt.words = p32;
+    if ((rc = stage_in(eng->nv_to, txt->offsets, txt->offsets ? (size_t)n + 1 : 0, st, &p32))) return rc;
+    dt.offsets = txt->offsets ? p32 : nullptr;
+    int32_t *ds = nullptr;
+    int16_t *ds16 = nullptr;
+    if (scores) { CK(eng->nv_s.reserve((size_t)n * 4)); ds = eng->nv_s.as<int32_t>(); }
+    if (scores16) { CK(eng->nv_s16.reserve((size_t)n * 2)); ds16 = eng->nv_s16.as<int16_t>(); }
+    rc = gx::nv_score_device(*al, n, dp, dt, ds, ds16, max_p, max_t, st);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    if (scores) CK(hipMemcpyAsync(scores, ds, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    if (scores16) CK(hipMemcpyAsync(scores16, ds16, (size_t)n * 2, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
     return GASALX_OK;
 }

@@ -97,6 +97,11 @@ int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *r
                          const float *ph2pr_dev, const uint32_t *perm, const HmmClass *classes, int n_classes,
                          uint32_t max_r, uint32_t max_h);
 
+// nvbio-style batched scoring (batched.hip, nvbio.hpp)
+int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
+                    const gasalx_nv_strings &txt, int32_t *scores, int16_t *scores16, uint32_t max_p, uint32_t max_t,
+                    hipStream_t stream);
+
 void set_error(const std::string &msg);
 const char *last_error();
 

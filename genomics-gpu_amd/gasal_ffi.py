@@ -32,7 +32,12 @@ EXPORTS = (
     "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
     "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
     "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
+    "gasalx_nv_score_device", "gasalx_nv_score_host",
 )
+
+# nvbio front-end (gasalx_nv_*): aligners and AlignmentType (nvbio/alignment/alignment_base.h:54)
+NV_ED, NV_SW, NV_GOTOH = 0, 1, 2
+NV_GLOBAL, NV_LOCAL, NV_SEMI_GLOBAL = 0, 1, 2
 
 
 class Params(ctypes.Structure):
@@ -77,6 +82,16 @@ class CHmmFile(ctypes.Structure):
                 ("base_quals", ctypes.c_void_p), ("ins_quals", ctypes.c_void_p), ("del_quals", ctypes.c_void_p),
                 ("gcp_quals", ctypes.c_void_p), ("haps", ctypes.c_void_p), ("hap_offsets", ctypes.c_void_p),
                 ("hap_lens", ctypes.c_void_p), ("read_bytes", ctypes.c_uint64), ("hap_bytes", ctypes.c_uint64)]
+
+
+class CNvAligner(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("aligner", "type", "match", "mismatch", "gap_open", "gap_ext",
+                                               "deletion", "insertion")]
+
+
+class CNvStrings(ctypes.Structure):
+    _fields_ = [("words", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("length", ctypes.c_uint32),
+                ("bits", ctypes.c_uint32), ("big_endian", ctypes.c_uint32)]
 
 
 _lib = None
@@ -307,6 +322,19 @@ class Engine:
         _check(lib().gasalx_pairhmm_quals_host(self._h, ctypes.byref(hb), _p(res)), "pairhmm_quals_host")
         return res
 
+    def nv_score_host(self, aligner: "NvAligner", patterns: "PackedSet", texts: "PackedSet", int16=False):
+        """nvbio-style batched scores (gasalx_nv_score_host): patterns[i] against texts[i]
+        (or the one shared text).  int16: also return sw-benchmark's int16 score vector."""
+        n = patterns.n
+        sc = np.zeros(n, np.int32)
+        s16 = np.zeros(n, np.int16) if int16 else None
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_score_host(self._h, ctypes.byref(ca), ctypes.c_uint32(n),
+                                          ctypes.byref(patterns.cstruct()), ctypes.c_uint64(len(patterns.words)),
+                                          ctypes.byref(texts.cstruct()), ctypes.c_uint64(len(texts.words)), _p(sc),
+                                          _p(s16)), "nv_score_host")
+        return (sc, s16) if int16 else sc
+
     def pairhmm_device_ptrs(self, ptrs: dict, read_bytes: int, hap_bytes: int, n: int, max_r: int, max_h: int,
                             result_ptr: int, stream: int = 0):
         g = lambda k: ptrs.get(k) or None
@@ -373,6 +401,83 @@ class HmmData:
     def float_params(self):
         """The reference host's four per-base parameters (tile_1.cu:415-419)."""
         return pairhmm_params(self.base_quals, self.ins_quals, self.del_quals)
+
+
+@dataclass
+class NvAligner:
+    """nvbio aligner + scoring scheme (make_gotoh_aligner / make_smith_waterman_aligner /
+    make_edit_distance_aligner; SimpleGotohScheme and SimpleSmithWatermanScheme, signed)."""
+    aligner: int
+    type: int
+    match: int = 0
+    mismatch: int = 0
+    gap_open: int = 0
+    gap_ext: int = 0
+    deletion: int = 0
+    insertion: int = 0
+
+    def cstruct(self):
+        return CNvAligner(self.aligner, self.type, self.match, self.mismatch, self.gap_open, self.gap_ext,
+                          self.deletion, self.insertion)
+
+    def prm(self):
+        return np.array([self.match, self.mismatch, self.gap_open, self.gap_ext, self.deletion, self.insertion],
+                        np.int32)
+
+
+@dataclass
+class PackedSet:
+    """An nvbio packed string set: `bits` per symbol, symbol 0 in the top bits of a word
+    when big_endian; offsets (n + 1 symbols) or None for one shared string of `length`."""
+    words: np.ndarray
+    offsets: np.ndarray | None
+    length: int
+    bits: int
+    big_endian: bool
+
+    @property
+    def n(self):
+        return 0 if self.offsets is None else len(self.offsets) - 1
+
+    def cstruct(self):
+        return CNvStrings(_p(self.words), _p(self.offsets), self.length, self.bits, int(self.big_endian))
+
+    @classmethod
+    def pack(cls, seqs, bits=4, big_endian=True, shared=False):
+        """seqs: sequences of symbol codes (each < 2**bits).  shared: one string (texts)."""
+        seqs = [np.asarray(s, np.uint32) for s in seqs]
+        lens = np.array([len(s) for s in seqs], np.uint64)
+        total = int(lens.sum())
+        per = 32 // bits
+        flat = np.concatenate(seqs) if seqs else np.zeros(0, np.uint32)
+        if flat.size and int(flat.max()) >= (1 << bits):
+            raise ValueError("symbol does not fit the packing")
+        idx = np.arange(total, dtype=np.uint64)
+        pos = (idx % per).astype(np.uint32)
+        shift = (32 - bits * (pos + 1)) if big_endian else bits * pos
+        words = np.zeros((total + per - 1) // per + 1, np.uint64)
+        np.add.at(words, (idx // per).astype(np.int64), flat.astype(np.uint64) << shift.astype(np.uint64))
+        words = words.astype(np.uint32)
+        if shared:
+            return cls(words, None, total, bits, big_endian)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+        return cls(words, offs, 0, bits, big_endian)
+
+
+# sw-benchmark's encodings (sw-benchmark.cu:290-330): reads as DNA_N (A0 C1 G2 T3, other 4),
+# the reference through nst_nt4_table with N (and every non-ACGT byte) stored as 0
+def dna_n_codes(seq) -> np.ndarray:
+    b = np.frombuffer(seq.encode() if isinstance(seq, str) else bytes(seq), np.uint8)
+    lut = np.full(256, 4, np.uint32)
+    for i, ch in enumerate(b"ACGT"):
+        lut[ch] = i
+        lut[ch + 32] = i
+    return lut[b]
+
+
+def ref2_codes(seq) -> np.ndarray:
+    c = dna_n_codes(seq)
+    return np.where(c < 4, c, 0).astype(np.uint32)
 
 
 def read_hmm_file(path: str) -> HmmData:

@@ -208,6 +208,50 @@ typedef struct gasalx_hmm_file {
 int gasalx_hmm_file_read(const char *path, gasalx_hmm_file **out);
 int gasalx_hmm_file_free(gasalx_hmm_file *f);
 
+/* Second front-end: nvbio-style batched alignment scoring (NvB/nvbio/alignment/
+ * batched.h:44-87, the BatchedAlignmentScore<stream, scheduler> idiom of
+ * sw-benchmark.cu:355-443; C++ wrapper in include/nvbio_batched.h).  nvbio's textbook
+ * recurrences, not GASAL2's: Gotoh (gotoh/gotoh_inl.h), Smith-Waterman with linear
+ * gaps (sw/sw_inl.h), edit distance (ed/ed_utils.h:45-52), each GLOBAL / LOCAL /
+ * SEMI_GLOBAL (pattern fully aligned, text ends free); the output is the BestSink
+ * score per pair. */
+enum { GASALX_NV_ED = 0, GASALX_NV_SW = 1, GASALX_NV_GOTOH = 2 };
+enum { GASALX_NV_GLOBAL = 0, GASALX_NV_LOCAL = 1, GASALX_NV_SEMI_GLOBAL = 2 };   /* nvbio AlignmentType */
+
+typedef struct gasalx_nv_aligner {
+    int32_t aligner;      /* GASALX_NV_ED / _SW / _GOTOH */
+    int32_t type;         /* GASALX_NV_GLOBAL / _LOCAL / _SEMI_GLOBAL */
+    int32_t match;        /* signed scores as in SimpleGotohScheme / SimpleSmithWatermanScheme */
+    int32_t mismatch;     /*   (utils.h:92-135): penalties are negative                        */
+    int32_t gap_open;     /* Gotoh: a gap of k symbols scores gap_open + (k-1) * gap_ext         */
+    int32_t gap_ext;
+    int32_t deletion;     /* Smith-Waterman: per text symbol skipped                            */
+    int32_t insertion;    /* Smith-Waterman: per pattern symbol skipped                         */
+} gasalx_nv_aligner;
+
+/* A packed string set (nvbio PackedStream): symbol s of the set is field s % (32/bits)
+ * of word s / (32/bits), counted from the top of the word when big_endian (nvbio reads,
+ * SequenceDataTraits SEQUENCE_BIG_ENDIAN) or from bit 0 otherwise (sw-benchmark's
+ * 2-bit reference, REF_BIG_ENDIAN = false). */
+typedef struct gasalx_nv_strings {
+    const uint32_t *words;
+    const uint32_t *offsets;  /* n + 1 symbol offsets; texts: NULL = one text of `length` symbols for every pair */
+    uint32_t length;
+    uint32_t bits;            /* 2, 4 or 8 */
+    uint32_t big_endian;
+} gasalx_nv_strings;
+
+/* scores (int32) and/or scores16 (int16, sw-benchmark's score vector) per pair.
+ * Patterns up to 1024 symbols; max lengths are upper bounds (0 = read back). */
+int gasalx_nv_score_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
+                           const gasalx_nv_strings *dev_patterns, const gasalx_nv_strings *dev_texts,
+                           int32_t *dev_scores, int16_t *dev_scores16, uint32_t max_pattern_len,
+                           uint32_t max_text_len, void *stream);
+/* Host arrays in and out (words: the number of words of each set). */
+int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
+                         const gasalx_nv_strings *patterns, uint64_t pattern_words, const gasalx_nv_strings *texts,
+                         uint64_t text_words, int32_t *scores, int16_t *scores16);
+
 /* Synthetic workloads of SURVEY.md §8(d) (benchmark/test data, std::mt19937_64).
  * Writes a GASAL2-layout batch (N_CODE padding) into caller buffers sized by
  * gasalx_synth_sizes.  kind: 1..4 = configs 1..4.  Pairs come in blocks of 65,536,

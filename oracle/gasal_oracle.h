@@ -84,6 +84,22 @@ int orc_pairhmm_batch(uint32_t n_pairs,
                       const uint8_t *haps, const uint32_t *hap_off, const uint32_t *hap_len,
                       float *result, int n_threads);
 
+/*
+ * nvbio batched alignment score (second front-end; nvbio_oracle.c).  aligner:
+ * ORC_NV_ED / _SW / _GOTOH; type: nvbio AlignmentType (GLOBAL 0, LOCAL 1, SEMI_GLOBAL 2).
+ * prm = {match, mismatch, gap_open, gap_ext, deletion, insertion} (signed).
+ * Strings are nvbio packed sets (bits per symbol, big-endian flag); toff NULL = one
+ * shared text of tlen0 symbols.  Returns the BestSink score per pair.
+ */
+enum { ORC_NV_ED = 0, ORC_NV_SW = 1, ORC_NV_GOTOH = 2 };
+enum { ORC_NV_GLOBAL = 0, ORC_NV_LOCAL = 1, ORC_NV_SEMI_GLOBAL = 2 };
+int32_t orc_nv_score_one(int aligner, int type, const int32_t prm[6], const uint32_t *pat, uint32_t M,
+                         const uint32_t *txt, uint32_t N);
+int orc_nv_score_batch(int aligner, int type, const int32_t prm[6], uint32_t n,
+                       const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                       const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
+                       int32_t *scores, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -113,3 +113,21 @@ def pairhmm(reads, read_off, read_len, qm, delta, xiksi, alpha, haps, hap_off, h
                             _ptr(c(hap_off, np.uint32)), _ptr(c(hap_len, np.uint32)), _ptr(res),
                             ctypes.c_int(n_threads))
     return res
+
+
+def nv_score(aligner, patterns, texts, n_threads=0):
+    """nvbio batched score restatement (nvbio_oracle.c): aligner is a gasal_ffi.NvAligner
+    (or anything with aligner/type/prm()), patterns/texts gasal_ffi.PackedSet-like."""
+    n = len(patterns.offsets) - 1
+    out = np.zeros(n, np.int32)
+    lib().orc_nv_score_batch.restype = ctypes.c_int
+    rc = lib().orc_nv_score_batch(ctypes.c_int(aligner.aligner), ctypes.c_int(aligner.type), _ptr(aligner.prm()),
+                                  ctypes.c_uint32(n), _ptr(patterns.words), _ptr(patterns.offsets),
+                                  ctypes.c_uint32(patterns.bits), ctypes.c_uint32(int(patterns.big_endian)),
+                                  _ptr(texts.words), _ptr(texts.offsets), ctypes.c_uint32(texts.length),
+                                  ctypes.c_uint32(texts.bits), ctypes.c_uint32(int(texts.big_endian)), _ptr(out),
+                                  ctypes.c_int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"orc_nv_score_batch failed ({rc})")
+    return out
+

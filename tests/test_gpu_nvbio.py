@@ -1,0 +1,156 @@
+"""GPU parity of the second front-end (nvbio-style batched scoring, include/nvbio_batched.h
+over gasalx_nv_*): the HIP kernels (nvbio.hpp) against the oracle restatement
+(oracle/nvbio_oracle.c) on the same packed string sets.  Scores are integers:
+bit-exact.  Covers the three aligners x three alignment types, shared and per-pair
+texts, 2/4/8-bit packings in both word orders, patterns up to 1024 symbols, the
+sw-benchmark driver (tools/sw_benchmark) end to end."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import gasal_ffi as G
+import helpers
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ALIGNERS = [G.NvAligner(G.NV_GOTOH, 0, 2, -1, -2, -1), G.NvAligner(G.NV_SW, 0, 2, -3, 0, 0, -2, -3),
+            G.NvAligner(G.NV_ED, 0), G.NvAligner(G.NV_GOTOH, 0, 5, -4, -10, -1)]
+
+
+def _al(base, type_):
+    return G.NvAligner(base.aligner, type_, base.match, base.mismatch, base.gap_open, base.gap_ext, base.deletion,
+                       base.insertion)
+
+
+def _related(rng, text, m):
+    if len(text) <= m:
+        return list(rng.integers(0, 4, m))
+    st = int(rng.integers(0, len(text) - m + 1))
+    p = list(text[st:st + m])
+    for k in range(m):
+        if rng.random() < 0.06:
+            p[k] = int(rng.integers(0, 5))
+    return p
+
+
+def _check(engine, al, P, T):
+    g = engine.nv_score_host(al, P, T)
+    o = O.nv_score(al, P, T)
+    bad = np.nonzero(g != o)[0]
+    assert bad.size == 0, f"{bad.size}/{len(g)} differ, first #{bad[0]}: gpu={g[bad[0]]} oracle={o[bad[0]]} {al}"
+    return g
+
+
+@pytest.mark.parametrize("base", ALIGNERS, ids=["gotoh", "sw", "ed", "gotoh_b"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_shared_text(engine, base, type_):
+    # the sw-benchmark layout: every read against one reference (2-bit LE), reads 4-bit BE DNA_N
+    rng = np.random.default_rng(7 * base.aligner + type_ + base.match)
+    text = list(rng.integers(0, 4, 1500))
+    pats = [np.array(_related(rng, text, int(rng.integers(1, 260))), np.uint32) for _ in range(700)]
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
+    _check(engine, _al(base, type_), P, T)
+
+
+@pytest.mark.parametrize("base", ALIGNERS[:3], ids=["gotoh", "sw", "ed"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_per_pair_texts(engine, base, type_):
+    rng = np.random.default_rng(100 + 7 * base.aligner + type_)
+    pats, texts = [], []
+    for _ in range(900):
+        t = list(rng.integers(0, 4, int(rng.integers(1, 400))))
+        texts.append(np.array(t, np.uint32))
+        pats.append(np.array(_related(rng, t, int(rng.integers(1, 200))), np.uint32))
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+    _check(engine, _al(base, type_), P, T)
+
+
+@pytest.mark.parametrize("bits,big", [(2, True), (2, False), (4, False), (8, True), (8, False)])
+def test_packings(engine, bits, big):
+    rng = np.random.default_rng(bits * 2 + big)
+    hi = 4 if bits == 2 else (16 if bits == 4 else 256)
+    pats = [rng.integers(0, hi, int(rng.integers(1, 150))).astype(np.uint32) for _ in range(400)]
+    texts = [rng.integers(0, hi, int(rng.integers(1, 300))).astype(np.uint32) for _ in range(400)]
+    for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+        _check(engine, _al(ALIGNERS[0], type_), G.PackedSet.pack(pats, bits, big), G.PackedSet.pack(texts, bits, big))
+
+
+@pytest.mark.parametrize("m", [8, 64, 65, 128, 129, 256, 257, 512, 513, 1024])
+def test_pattern_lengths_every_shape(engine, m):
+    # lane-group shapes (8,8) (8,16) (16,16) (32,16) (64,16) of batched.hip, at their edges
+    rng = np.random.default_rng(m)
+    text = list(rng.integers(0, 4, 2200))
+    pats = [np.array(_related(rng, text, m - int(rng.integers(0, 3))), np.uint32) for _ in range(96)]
+    T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
+    for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+        _check(engine, _al(ALIGNERS[0], type_), G.PackedSet.pack(pats), T)
+
+
+def test_empty_and_positive_scores(engine):
+    # empty patterns / texts, and a scheme whose gaps score > 0 (LOCAL pads then masked)
+    rng = np.random.default_rng(3)
+    pats = [np.zeros(0, np.uint32), rng.integers(0, 4, 5).astype(np.uint32), np.zeros(0, np.uint32),
+            rng.integers(0, 4, 30).astype(np.uint32)]
+    texts = [rng.integers(0, 4, 9).astype(np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint32),
+             rng.integers(0, 4, 70).astype(np.uint32)]
+    P, T = G.PackedSet.pack(pats, 4), G.PackedSet.pack(texts, 2, False)
+    for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+        for al in ALIGNERS:
+            _check(engine, _al(al, type_), P, T)
+        _check(engine, G.NvAligner(G.NV_SW, type_, 1, 2, 0, 0, 1, -1), P, T)
+        _check(engine, G.NvAligner(G.NV_GOTOH, type_, 1, -1, 1, 1), P, T)
+
+
+def test_int16_scores(engine):
+    rng = np.random.default_rng(11)
+    text = list(rng.integers(0, 4, 900))
+    pats = [np.array(_related(rng, text, 150), np.uint32) for _ in range(300)]
+    P = G.PackedSet.pack(pats)
+    T = G.PackedSet.pack([np.array(text, np.uint32)], 2, False, shared=True)
+    al = _al(ALIGNERS[0], G.NV_GLOBAL)
+    s32, s16 = engine.nv_score_host(al, P, T, int16=True)
+    assert np.array_equal(s16, s32.astype(np.int16))
+    assert np.array_equal(s32, O.nv_score(al, P, T))
+
+
+def test_sw_benchmark_driver(tmp_path):
+    # tools/sw_benchmark (client of include/nvbio_batched.h): FASTQ reads against a FASTA
+    # reference, every int16 score of every test against the oracle
+    rng = np.random.default_rng(0x5B)
+    ref = helpers.random_seq(rng, 1200).decode()
+    reads = []
+    for _ in range(1500):
+        m = int(rng.integers(50, 151))
+        st = int(rng.integers(0, len(ref) - m))
+        r = bytearray(ref[st:st + m].encode())
+        for k in range(m):
+            if rng.random() < 0.05:
+                r[k] = b"ACGTN"[int(rng.integers(0, 5))]
+        reads.append(r.decode())
+    fq = tmp_path / "reads.fq"
+    fq.write_text("".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(reads)))
+    fa = tmp_path / "ref.fa"
+    fa.write_text(">ref\n" + "\n".join(ref[i:i + 60] for i in range(0, len(ref), 60)) + "\n")
+    out = tmp_path / "scores.tsv"
+    prog = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "sw_benchmark")
+    r = subprocess.run([prog, "-tests", "gotoh:ed:sw", "-scores", str(out), str(fq), str(fa)], capture_output=True,
+                       text=True, check=True)
+    assert "GCUPS" in r.stderr
+    got = {}
+    for line in out.read_text().splitlines():
+        test, name, i, v = line.split("\t")
+        got.setdefault((test, name), []).append(int(v))
+    P = G.PackedSet.pack([G.dna_n_codes(s) for s in reads], 4, True)
+    T = G.PackedSet.pack([G.ref2_codes(ref)], 2, False, shared=True)
+    cases = {("gotoh", "global"): G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2, -1, -2, -1),
+             ("gotoh", "semi-global"): G.NvAligner(G.NV_GOTOH, G.NV_SEMI_GLOBAL, 2, -1, -2, -1),
+             ("gotoh", "local"): G.NvAligner(G.NV_GOTOH, G.NV_LOCAL, 2, -1, -2, -1),
+             ("ed", "semi-global"): G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL),
+             ("sw", "local"): G.NvAligner(G.NV_SW, G.NV_LOCAL, 2, -1, 0, 0, -1, -1)}
+    for key, al in cases.items():
+        assert np.array_equal(np.array(got[key], np.int16), O.nv_score(al, P, T).astype(np.int16)), key

@@ -1,0 +1,118 @@
+"""CPU checks of the nvbio front-end's oracle (oracle/nvbio_oracle.c), the checker of
+the second front-end (include/nvbio_batched.h).  nvbio needs CUDA + thrust, so it
+cannot run here: the restatement is pinned by hand-derived known answers (each
+worked out below from the recurrences of gotoh/gotoh_inl.h, sw/sw_inl.h and
+ed/ed_utils.h) and cross-checked against an independent textbook DP written here
+in plain Python (full matrices, no stripes)."""
+import numpy as np
+import pytest
+
+import gasal_ffi as G
+import oracle as O
+
+GOTOH = (2, -1, -2, -1)   # sw-benchmark.cu:587-591
+
+
+def score(al, p, t):
+    P = G.PackedSet.pack([G.dna_n_codes(p)])
+    T = G.PackedSet.pack([G.ref2_codes(t)], bits=2, big_endian=False)
+    return int(O.nv_score(al, P, T)[0])
+
+
+def gotoh(type_, p, t, s=GOTOH):
+    return score(G.NvAligner(G.NV_GOTOH, type_, *s), p, t)
+
+
+# Gotoh known answers, scheme (match 2, mismatch -1, gap open -2, gap extend -1): a gap of
+# k symbols scores -2 - (k - 1) (F = max(F + Ge, H + Go), gotoh_inl.h:1029-1037)
+KATS = [
+    # type, pattern, text, expected, derivation
+    (G.NV_GLOBAL, "ACGT", "ACGT", 8, "4 matches"),
+    (G.NV_GLOBAL, "ACGT", "AGT", 4, "A C- G T: 3 matches (6), one pattern gap (-2)"),
+    (G.NV_GLOBAL, "AAAA", "A", -2, "1 match (2), gap of 3 (-4)"),
+    (G.NV_GLOBAL, "ACGTTTTACGT", "ACGTACGT", 12, "8 matches (16), gap of 3 (-4)"),
+    (G.NV_GLOBAL, "TTACGT", "ACGT", 5, "leading gap of 2 (-3), 4 matches (8): textbook boundary"),
+    (G.NV_SEMI_GLOBAL, "CGT", "AACGTAA", 6, "free text ends, 3 matches"),
+    (G.NV_SEMI_GLOBAL, "CGTT", "AACGTAA", 5, "CGT + T/A mismatch: 6 - 1"),
+    (G.NV_LOCAL, "GGACGTGG", "TTACGTTT", 8, "ACGT, flanks mismatch"),
+    (G.NV_LOCAL, "TTTT", "GGGG", 0, "no match: the 0 clamp"),
+]
+
+
+@pytest.mark.parametrize("type_,p,t,expected,why", KATS)
+def test_gotoh_known_answers(type_, p, t, expected, why):
+    assert gotoh(type_, p, t) == expected, why
+
+
+def test_sw_and_ed_known_answers():
+    sw = G.NvAligner(G.NV_SW, G.NV_GLOBAL, match=1, mismatch=-1, deletion=-1, insertion=-1)
+    assert score(sw, "ACGT", "ACT") == 2                     # A C G- T: 3 - 1
+    sw_local = G.NvAligner(G.NV_SW, G.NV_LOCAL, match=2, mismatch=-3, deletion=-5, insertion=-5)
+    assert score(sw_local, "ACGT", "TTACGTTT") == 8
+    ed = lambda t_: G.NvAligner(G.NV_ED, t_)
+    assert score(ed(G.NV_GLOBAL), "ACGTACGT", "ACGTTCGT") == -1     # one substitution
+    assert score(ed(G.NV_GLOBAL), "ACGT", "ACGTAA") == -2           # two text symbols deleted
+    assert score(ed(G.NV_SEMI_GLOBAL), "GTA", "ACGTACG") == 0       # exact substring
+    assert score(ed(G.NV_SEMI_GLOBAL), "GTTA", "ACGTACG") == -1     # one insertion
+    assert score(ed(G.NV_LOCAL), "ACGT", "TTTT") == 0               # match 0, the 0 clamp
+
+
+def test_empty_pattern_and_text():
+    # M = 0: only the band initialisation reaches the sink (gotoh_inl.h:1188, 1403-1420)
+    P0 = G.PackedSet.pack([np.zeros(0, np.uint32)])
+    T5 = G.PackedSet.pack([G.ref2_codes("ACGTA")], bits=2, big_endian=False)
+    assert int(O.nv_score(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, *GOTOH), P0, T5)[0]) == -2 - 4
+    assert int(O.nv_score(G.NvAligner(G.NV_GOTOH, G.NV_SEMI_GLOBAL, *GOTOH), P0, T5)[0]) == 0
+    assert int(O.nv_score(G.NvAligner(G.NV_GOTOH, G.NV_LOCAL, *GOTOH), P0, T5)[0]) == -2 ** 31
+    assert int(O.nv_score(G.NvAligner(G.NV_SW, G.NV_GLOBAL, 1, -1, 0, 0, -3, -3), P0, T5)[0]) == -15
+
+
+# ---- independent textbook DP (full matrices) ----
+def textbook(aligner, type_, p, t, s):
+    M, N = len(p), len(t)
+    NEG = -10 ** 9
+    match, mism, go, ge, de, ins = s
+    if aligner == G.NV_ED:
+        match, mism, de, ins = 0, -1, -1, -1
+    H = [[0] * (N + 1) for _ in range(M + 1)]
+    E = [[NEG] * (N + 1) for _ in range(M + 1)]
+    F = [[NEG] * (N + 1) for _ in range(M + 1)]
+    gotoh_ = aligner == G.NV_GOTOH
+    for j in range(1, N + 1):   # row -1: text prefix skipped
+        H[0][j] = (go + ge * (j - 1) if gotoh_ else de * j) if type_ == G.NV_GLOBAL else 0
+    for i in range(1, M + 1):   # column -1: pattern prefix skipped
+        H[i][0] = (go + ge * (i - 1) if gotoh_ else ins * i) if type_ != G.NV_LOCAL else 0
+    best = -2 ** 31
+    for i in range(1, M + 1):
+        for j in range(1, N + 1):
+            sc = match if p[i - 1] == t[j - 1] else mism
+            if gotoh_:
+                F[i][j] = max(F[i - 1][j] + ge, H[i - 1][j] + go)
+                E[i][j] = max(E[i][j - 1] + ge, H[i][j - 1] + go)
+                h = max(E[i][j], F[i][j], H[i - 1][j - 1] + sc)
+            else:
+                h = max(H[i - 1][j] + ins, H[i][j - 1] + de, H[i - 1][j - 1] + sc)
+            if type_ == G.NV_LOCAL:
+                h = max(h, 0)
+                best = max(best, h)
+            H[i][j] = h
+    if type_ == G.NV_SEMI_GLOBAL and M and N:
+        best = max(H[M][1:])
+    if type_ == G.NV_GLOBAL and M and N:
+        best = H[M][N]
+    return best
+
+
+@pytest.mark.parametrize("aligner", [G.NV_ED, G.NV_SW, G.NV_GOTOH])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL])
+def test_oracle_matches_textbook_dp(aligner, type_):
+    rng = np.random.default_rng(1000 * aligner + type_)
+    s = (2, -1, -2, -1, -1, -1) if aligner == G.NV_GOTOH else (2, -3, 0, 0, -2, -3)
+    for _ in range(60):
+        M, N = int(rng.integers(1, 30)), int(rng.integers(1, 40))
+        p = list(rng.integers(0, 5, M))       # DNA_N codes incl. N = 4 (never matches the 2-bit text)
+        t = list(rng.integers(0, 4, N))
+        al = G.NvAligner(aligner, type_, *s)
+        P = G.PackedSet.pack([np.array(p, np.uint32)], bits=4)
+        T = G.PackedSet.pack([np.array(t, np.uint32)], bits=2, big_endian=False)
+        assert int(O.nv_score(al, P, T)[0]) == textbook(aligner, type_, p, t, s)
