@@ -155,8 +155,11 @@ __global__ __launch_bounds__(256) void nv_kernel(NvArgs A) {
                 else if ((uint32_t)c == N - 1) best = h;
             }
         }
+        // hand the bottom row down: H(r0+R-1, c) once active; before that Hk[R-1] still
+        // holds the row's left boundary H(r0+R-1, -1), the diagonal the lane below needs
+        // at its column 0
         pH = rH;
-        rH = nv_shr(Hup);
+        rH = nv_shr(Hk[R - 1]);
         rF = nv_shr(Fup);
     }
     // LOCAL: the pair's best over its lanes
