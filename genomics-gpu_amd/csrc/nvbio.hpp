@@ -111,7 +111,12 @@ __global__ __launch_bounds__(256) void nv_kernel(NvArgs A) {
     const uint32_t nsteps = nmax + G - 1;
     const uint32_t last_lane = M ? (M - 1) / R : 0, last_k = M ? (M - 1) - last_lane * R : 0;
     int32_t best = INT32_MIN;                     // BestSink() (sink_inl.h:38-40)
-    int32_t rH = 0, rF = kNvInf, pH = 0;          // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1)
+    // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1).  rH starts as the left
+    // boundary H(r0-1, -1): lane 1 takes it as its diagonal at column 0 (lane 0 never
+    // runs a column -1 step to hand it down)
+    const int32_t rb = (int32_t)r0 - 1;
+    int32_t rH = (TYPE == NV_LOCAL || lg == 0) ? 0 : (GOTOH ? A.go + A.ge * rb : A.ins * (rb + 1));
+    int32_t rF = kNvInf, pH = 0;
     for (uint32_t s = 0; s < nsteps; ++s) {
         const int32_t c = (int32_t)s - (int32_t)lg;
         int32_t Hup, Fup, Hdg;
