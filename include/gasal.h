@@ -4,8 +4,11 @@
  * Drop-in for Non-CDP/GASAL2/src/gasal.h:1-168 (reference).  Names, enum
  * values and struct field order are identical so that code written against the
  * reference (e.g. test_prog.cpp) compiles unchanged; the only substitution is
- * cudaStream_t -> hipStream_t (both opaque pointers, same layout), and
- * CHECKCUDAERROR -> CHECKHIPERROR.  uint4 comes from the HIP vector types.
+ * cudaStream_t -> hipStream_t (both opaque pointers, same layout).  The
+ * reference's error helpers keep their names (CHECKCUDAERROR assigns to the
+ * caller's `err`, as gasal.h:15-22 does; CudaCheckKernelLaunch, :25-34) and
+ * check HIP status codes; CHECKHIPERROR is the self-contained form.  uint4 comes
+ * from the HIP vector types.
  */
 #ifndef __GASAL_H__
 #define __GASAL_H__
@@ -31,6 +34,22 @@
             exit(EXIT_FAILURE);                                                              \
         }                                                                                    \
     } while (0)
+
+/* gasal.h:15-22 under its own name: `err` is the caller's status variable (hipError_t). */
+#define CHECKCUDAERROR(error)                                                                \
+    do {                                                                                     \
+        err = (error);                                                                       \
+        if (hipSuccess != err) {                                                             \
+            fprintf(stderr, "[GASAL CUDA ERROR:] %s(CUDA error no.=%d). Line no. %d in file %s\n", \
+                    hipGetErrorString(err), (int)err, __LINE__, __FILE__);                   \
+            exit(EXIT_FAILURE);                                                              \
+        }                                                                                    \
+    } while (0)
+
+/* gasal.h:25-34: -1 when the last launch failed. */
+inline int CudaCheckKernelLaunch() {
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 enum comp_start {
     WITHOUT_START,

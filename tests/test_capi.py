@@ -149,3 +149,14 @@ def test_pinned_host_lifetime_follows_its_arrays():
     del view
     gc.collect()
     assert ref() is None
+
+
+def test_reference_error_helpers_compile(tmp_path):
+    # a caller written against the reference's gasal.h error helpers (gasal.h:15-34)
+    # compiles unchanged against include/gasal_header.h
+    src = tmp_path / "caller.cpp"
+    src.write_text('#include "gasal_header.h"\n'
+                   "int f() { hipError_t err; CHECKCUDAERROR(hipGetLastError());\n"
+                   "          return CudaCheckKernelLaunch(); }\n")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-c", str(src), "-o",
+                    str(tmp_path / "caller.o")], check=True, capture_output=True)
