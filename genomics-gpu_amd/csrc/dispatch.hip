@@ -612,9 +612,9 @@ static int pairhmm_launch(HmmArgs A, bool quals, int G, uint32_t slot0, uint32_t
     A.slot0 = slot0;
     A.n = slot1;
     A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
+    HmmFn fn = quals ? hmm_lookup<true>(G) : hmm_lookup<false>(G);
     const size_t lds = (size_t)4 * (64 / G) * A.lds_stride;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
-    HmmFn fn = quals ? hmm_lookup<true>(G) : hmm_lookup<false>(G);
     if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);
     HIPCHK(hipGetLastError());

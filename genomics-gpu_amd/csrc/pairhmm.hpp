@@ -36,7 +36,6 @@ struct HmmArgs {
 __device__ __forceinline__ float shr_lane_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
 }
-
 template <int G, int RR, bool QUALS = false>
 __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -115,31 +114,50 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     float acc = 0.f;
     float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
 
-    for (uint32_t s = 0; s < nsteps; ++s) {
+    // one column j of the lane's rows; (MU, IU, DU) in = row r0-1, out = the lane's bottom row
+    auto column = [&](uint32_t hb, float &MU, float &IU, float &DU) {
+#pragma unroll
+        for (int k = 0; k < RR; ++k) {
+            const float MID = __fadd_rn(IU, DU);                   // :149-162
+            const float DDM = __fmul_rn(Mk[k], xi[k]);
+            const float IIMI = __fmul_rn(IU, c01);
+            const float aa = (hb == rb[k]) ? qm1[k] : qm3[k];
+            const float MIIDD = __fmul_rn(c09, MID);
+            const float Mn = __fmul_rn(aa, MM[k]);
+            const float In = __fmaf_rn(MU, de[k], IIMI);
+            const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
+            MM[k] = __fmaf_rn(al[k], MU, MIIDD);
+            Mk[k] = Mn; Dk[k] = Dn;
+            MU = Mn; IU = In; DU = Dn;
+        }
+    };
+    auto checked_step = [&](uint32_t s) {
         const int32_t j = (int32_t)s - (int32_t)lg;
         float MU, IU, DU;
         if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }                  // row -1: M=I=0, D=D0
         else { MU = rM; IU = rI; DU = rD; }
-        const bool active = valid && j >= 0 && (uint32_t)j < H;
-        if (active) {
-            const uint32_t hb = hap[j];
-#pragma unroll
-            for (int k = 0; k < RR; ++k) {
-                const float MID = __fadd_rn(IU, DU);                   // :149-162
-                const float DDM = __fmul_rn(Mk[k], xi[k]);
-                const float IIMI = __fmul_rn(IU, c01);
-                const float aa = (hb == rb[k]) ? qm1[k] : qm3[k];
-                const float MIIDD = __fmul_rn(c09, MID);
-                const float Mn = __fmul_rn(aa, MM[k]);
-                const float In = __fmaf_rn(MU, de[k], IIMI);
-                const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
-                MM[k] = __fmaf_rn(al[k], MU, MIIDD);
-                Mk[k] = Mn; Dk[k] = Dn;
-                MU = Mn; IU = In; DU = Dn;
-            }
+        if (valid && j >= 0 && (uint32_t)j < H) {
+            column(hap[j], MU, IU, DU);
             if (bottom) acc = __fadd_rn(acc, __fadd_rn(MU, IU));       // row R-1, column j (:166-167)
         }
         rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+    };
+    {
+        // steps [G-1, hmin): every lane of the wave is inside its pair's columns, so
+        // no activity test and no merge of state
+        uint32_t hmin = valid ? H : 0u;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) hmin = min(hmin, (uint32_t)__shfl_xor(hmin, m));
+        const uint32_t s1 = min((uint32_t)G - 1, nsteps), s2 = max(s1, hmin);
+        for (uint32_t s = 0; s < s1; ++s) checked_step(s);
+        for (uint32_t s = s1; s < hmin; ++s) {
+            float MU = rM, IU = rI, DU = rD;
+            if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }
+            column(hap[s - lg], MU, IU, DU);
+            acc = __fadd_rn(acc, __fadd_rn(MU, IU));                   // kept by the bottom lane only
+            rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+        }
+        for (uint32_t s = s2; s < nsteps; ++s) checked_step(s);
     }
     if (valid && bottom) A.result[pair] = acc;
 }
