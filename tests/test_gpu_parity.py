@@ -771,3 +771,27 @@ def test_pairhmm_prog_driver(tmp_path):
     lines = [l for l in out.splitlines() if l.startswith("  i=")]
     assert len(lines) == 2 and lines[0].startswith("  i=999")
     np.testing.assert_allclose(float(lines[0].split()[1]), _hmm_oracle(d)[0], rtol=1e-5)
+
+
+def test_host_pipeline_cigar_overflow_at_chunk_edge(engine):
+    """SURVEY Q14 at a chunk boundary of gasalx_align_host's pipeline:
+    the last pair of chunk 0 has a CIGAR longer than its slot (1 query base against 600
+    target bases: ten 63-capped D runs around one M).  Scores, n_ops and every pair's own
+    slot bytes match the oracle (which writes pairs in order); only the residue in the
+    neighbour's slot may differ."""
+    rng = np.random.default_rng(0x91A1)
+    qs, ts = helpers.random_pairs(rng, 40000, 8, 72, 8, 80)
+    qs[19999], ts[19999] = b"A", helpers.random_seq(rng, 600, b"C")
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
+    b = G.Batch.from_pairs(qs, ts)
+    gp, op = _params_pair(**kw)
+    g = engine.align_host(b, gp)
+    o = O.align(b, op)
+    assert o["n_ops"][19999] > 8
+    assert np.array_equal(g["score"], o["score"]) and np.array_equal(g["n_ops"], o["n_ops"])
+    slot = (b.q_lens.astype(np.int64) + 7) // 8 * 8
+    for k in range(b.n):
+        m = int(min(o["n_ops"][k], slot[k]))
+        off = int(b.q_offsets[k])
+        if not np.array_equal(g["cigar"][off:off + m], o["cigar"][off:off + m]):
+            raise AssertionError(f"pair {k}: own-slot CIGAR bytes differ")
