@@ -77,15 +77,20 @@ WORKLOADS = {
     "pairhmm": dict(kind=5, pairs=100_000, scaling="weak", params=None, bytes=4762, ops=11,
                     label="config5: PairHMM fp32 forward, 100K reads x haplotypes (250 x 500) per GPU, "
                           "seed 0x5EED0005"),
+    "nvbio_gotoh": dict(kind=6, pairs=262_144, scaling="weak", params=None, bytes=88, ops=9,
+                        label="second front-end (nvbio BatchedAlignmentScore idiom, sw-benchmark.cu:585-615): "
+                              "Gotoh (2,-1,-2,-1) semi-global, 256K 150bp reads (4-bit DNA_N) per GPU against one "
+                              "1,000bp 2-bit reference, seed 0x5EED0006"),
     "cpu_plumbing": dict(kind=1, pairs=1024, scaling="weak", params=dict(algo=G.LOCAL), bytes=152, ops=12,
                          label="config1: 1024 pairs 64x64 SW local through the host-side CPU verify scorer "
                                "(oracle/), same batch through the GPU, seed 0x5EED0001"),
 }
 METRICS = {
     "pairhmm": "GCUPS of PairHMM fp32 forward (config 5, 250x500) on MI355X",
+    "nvbio_gotoh": "GCUPS of nvbio-style batched Gotoh semi-global scoring (sw-benchmark idiom) on MI355X",
     "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
 }
-SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005}
+SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006}
 
 
 def parse():
@@ -154,7 +159,47 @@ def synth_pairhmm(start, n, seed, rl=250, hl=500):
     qm, de, xi, al = G.pairhmm_params(bq, iq, iq)
     return dict(reads=reads.reshape(-1), read_offsets=np.arange(n, dtype=np.uint32) * rl,
                 read_lens=np.full(n, rl, np.uint32), qm=qm, delta=de, xiksi=xi, alpha=al, haps=haps.reshape(-1),
-                hap_offsets=np.arange(n, dtype=np.uint32) * hl, hap_lens=np.full(n, hl, np.uint32))
+                hap_offsets=np.arange(n, dtype=np.uint32) * hl, hap_lens=np.full(n, hl, np.uint32), bq=bq, iq=iq)
+
+
+NV_REF_LEN, NV_READ_LEN = 1000, 150
+NV_ALIGNER = dict(aligner=G.NV_GOTOH, type=G.NV_SEMI_GLOBAL, match=2, mismatch=-1, gap_open=-2, gap_ext=-1)
+
+
+def pack_uniform(codes, bits, big):
+    """nvbio PackedStream words of a flat symbol array (fast path of G.PackedSet.pack)."""
+    per = 32 // bits
+    flat = np.concatenate([codes.astype(np.uint32), np.zeros((-len(codes)) % per + per, np.uint32)])
+    k = np.arange(per, dtype=np.uint32)
+    shift = (32 - bits * (k + 1)) if big else bits * k
+    return np.bitwise_or.reduce(flat.reshape(-1, per) << shift, axis=1).astype(np.uint32)
+
+
+def synth_nvbio(start, n, seed):
+    """Reads of 150 bp taken from a 1,000 bp random reference at uniform offsets with
+    5% substitutions (N included, as DNA_N reads carry them); blocks of 8,192 reads
+    from default_rng((seed, block)) so a rank generates only its shard.  Codes:
+    reads DNA_N 4-bit big-endian, reference 2-bit little-endian (sw-benchmark.cu:73-74, 290-330)."""
+    ref = np.random.default_rng((seed, 1 << 40)).integers(0, 4, NV_REF_LEN).astype(np.uint32)
+    reads = []
+    b0, b1 = start // PH_BLOCK, (start + n + PH_BLOCK - 1) // PH_BLOCK
+    for b in range(b0, b1):
+        rng = np.random.default_rng((seed, b))
+        st = rng.integers(0, NV_REF_LEN - NV_READ_LEN + 1, PH_BLOCK)
+        rd = ref[st[:, None] + np.arange(NV_READ_LEN)[None, :]].copy()
+        sub = rng.random(rd.shape) < 0.05
+        rd[sub] = rng.integers(0, 5, int(sub.sum()))
+        lo, hi = max(start, b * PH_BLOCK) - b * PH_BLOCK, min(start + n, (b + 1) * PH_BLOCK) - b * PH_BLOCK
+        reads.append(rd[lo:hi])
+    codes = np.concatenate(reads).reshape(-1)
+    pat = G.PackedSet(pack_uniform(codes, 4, True), np.arange(n + 1, dtype=np.uint32) * NV_READ_LEN, 0, 4, True)
+    txt = G.PackedSet(pack_uniform(ref, 2, False), None, NV_REF_LEN, 2, False)
+    return dict(codes=codes, pat=pat, txt=txt)
+
+
+def nv_subset(nv, e):
+    codes = nv["codes"][:e * NV_READ_LEN]
+    return G.PackedSet(pack_uniform(codes, 4, True), np.arange(e + 1, dtype=np.uint32) * NV_READ_LEN, 0, 4, True)
 
 
 def ph_subset(h, e):
@@ -216,12 +261,20 @@ def cells_of(batch):
 
 def single_core_rate(O, kind, data, pkw, budget_s):
     """The oracle on 1 thread over a prefix of the rank-0 shard, bounded by budget_s."""
-    chunk = 256 if kind == 5 else 4096
+    chunk = 256 if kind in (5, 6) else 4096
     done, cells, used = 0, 0, 0.0
-    n = len(data["read_lens"]) if kind == 5 else data.n
+    n = len(data["read_lens"]) if kind == 5 else (len(data["pat"].offsets) - 1 if kind == 6 else data.n)
     while used < budget_s and done < n:
         e = min(done + chunk, n)
-        if kind == 5:
+        if kind == 6:
+            codes = data["codes"][done * NV_READ_LEN:e * NV_READ_LEN]
+            sub = G.PackedSet(pack_uniform(codes, 4, True), np.arange(e - done + 1, dtype=np.uint32) * NV_READ_LEN,
+                              0, 4, True)
+            t0 = time.perf_counter()
+            O.nv_score(G.NvAligner(**NV_ALIGNER), sub, data["txt"], n_threads=1)
+            used += time.perf_counter() - t0
+            cells += (e - done) * NV_READ_LEN * NV_REF_LEN
+        elif kind == 5:
             sub = {k: (v[done * 250:e * 250] if k in ("reads", "qm", "delta", "xiksi", "alpha")
                        else v[done * 500:e * 500] if k == "haps" else v[done:e]) for k, v in data.items()}
             sub["read_offsets"] = sub["read_offsets"] - sub["read_offsets"][0]
@@ -275,7 +328,10 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
     """PCIe-inclusive rate through the host-buffer entry point (gasalx_align_host /
     gasalx_pairhmm_host): host arrays in, H2D + kernels + D2H, results back in host
     arrays.  Reported beside `value`, never as it."""
-    if kind == 5:
+    if kind == 6:
+        call = lambda: eng.nv_score_host(G.NvAligner(**NV_ALIGNER), data["pat"], data["txt"])
+        path = "gasalx_nv_score_host (pageable host arrays; H2D + kernel + D2H)"
+    elif kind == 5:
         h = data
         args = (h["reads"], h["read_offsets"], h["read_lens"], h["qm"], h["delta"], h["xiksi"], h["alpha"],
                 h["haps"], h["hap_offsets"], h["hap_lens"])
@@ -301,12 +357,24 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
     dt, times = timed(call)
     res = {"value": round(cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_batch": round(dt * 1e3, 3),
            "ms_all": [round(t * 1e3, 3) for t in times], "path": path}
+    if kind == 5 and "bq" in data:
+        # the quality-input path (reference input terms: 4 bytes per read base instead of 17)
+        h = data
+        hd = G.HmmData(h["reads"], h["read_offsets"], h["read_lens"], h["bq"], h["iq"], h["iq"],
+                       np.zeros(0, np.uint8), h["haps"], h["hap_offsets"], h["hap_lens"],
+                       np.array([len(h["read_lens"])], np.uint32))
+        dtq, _ = timed(lambda: eng.pairhmm_quals_host(hd))
+        res["quals_host"] = {"value": round(cells / dtq / 1e9, 2), "ms_per_batch": round(dtq * 1e3, 3),
+                             "path": "gasalx_pairhmm_quals_host (read + 3 quality bytes per base in; ph2pr "
+                                     "parameters formed on the device; length-sorted classes)"}
+    if kind in (5, 6):
+        return res
     if kind != 5 and params.start_pos == G.WITH_TB:
         host = G.PinnedHost(data.q_bytes)
         dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, cigar_out=host.array))
         host.close()
         res["pinned_cigar"] = {"value": round(cells / dtp / 1e9, 2), "ms_per_batch": round(dtp * 1e3, 3)}
-    if kind != 5:
+    if True:
         # sequence bytes page-locked too, as the reference's host batch pages are
         # (host_batch.cpp:79-153 fills pinned pages), plus the CIGAR buffer for TB
         hq, ht = G.PinnedHost(data.q_bytes), G.PinnedHost(data.t_bytes)
@@ -326,6 +394,8 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
 def dtype_label(plan, kind):
     if kind == 5:
         return "fp32"
+    if kind == 6:
+        return "int32"
     if plan.startswith("wavefront16"):
         return "int16x2 packed (exact value window), int32 fallback per declined block"
     if plan.startswith("wavefront_"):
@@ -387,6 +457,8 @@ def main():
     seed = SEEDS[kind]
     if kind == 5:
         rl, hl = 250, 500
+    elif kind == 6:
+        rl, hl = NV_READ_LEN, NV_REF_LEN
     else:
         rl, hl = G.synth_spec(kind)
     shards = D.all_shards(n_global, rl, hl, world)
@@ -411,7 +483,25 @@ def main():
     gather = D.ScoreGather(counts, world, dev, dtype=torch.float32 if kind == 5 else torch.int32) \
         if do_gather else None
     t_syn = time.perf_counter()
-    if kind == 5:
+    if kind == 6:
+        nv = synth_nvbio(start, n, seed)
+        data = nv
+        cells_per_step = n * rl * hl
+        al = G.NvAligner(**NV_ALIGNER)
+        dpw = torch.from_numpy(nv["pat"].words.view(np.int32)).to(dev)
+        dpo = torch.from_numpy(nv["pat"].offsets.view(np.int32)).to(dev)
+        dtw = torch.from_numpy(nv["txt"].words.view(np.int32)).to(dev)
+        result = gather.buf if gather else torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        pat = {"words": dpw.data_ptr(), "offsets": dpo.data_ptr(), "bits": 4, "big_endian": True}
+        txt = {"words": dtw.data_ptr(), "offsets": 0, "length": NV_REF_LEN, "bits": 2, "big_endian": False}
+        plan = "nvbio gotoh semi-global, lane groups of 16 x 16 rows (batched.hip)"
+
+        def align():
+            eng.nv_score_device_ptrs(al, n, pat, txt, result.data_ptr(), 0, rl, hl, stream.cuda_stream)
+
+        def results():
+            return {"score": result[:n].cpu().numpy()}
+    elif kind == 5:
         h = synth_pairhmm(start, n, seed)
         data = h
         cells_per_step = int(np.sum(h["read_lens"].astype(np.int64) * h["hap_lens"].astype(np.int64)))
@@ -507,7 +597,12 @@ def main():
         m = min(n, args.parity_pairs)
         got = results()
         t_o = time.perf_counter()
-        if kind == 5:
+        if kind == 6:
+            ref = O.nv_score(G.NvAligner(**NV_ALIGNER), nv_subset(data, m), data["txt"], n_threads=threads)
+            mism = {"score": int(np.count_nonzero(got["score"][:m] != ref))}
+            extra = {}
+            ref_scores = ref
+        elif kind == 5:
             ref = oracle_pairhmm(O, ph_subset(data, m), threads)
             g_ = got["result"][:m]
             rel = np.abs(g_.astype(np.float64) - ref) / np.maximum(np.abs(ref.astype(np.float64)), 1e-30)
@@ -547,6 +642,7 @@ def main():
         parity = {"pairs_checked": int(tot[0]), "mismatches": int(tot[1]),
                   "by_field_rank0": mism, **extra,
                   "tolerance": "rtol 1e-5" if kind == 5 else "bit-exact",
+                  **({"oracle": "oracle/nvbio_oracle.c (nvbio semantics)"} if kind == 6 else {}),
                   "against": "oracle/ (CPU restatement of the reference kernels), on the timed steps' outputs"}
         if gather is not None:
             parity["gathered_scores_checked"] = int(sum(min(c, args.parity_pairs) for c in counts))
@@ -578,10 +674,18 @@ def main():
                 pmc = None
         same = pmc is not None and pmc.get("pairs_per_launch") == n
         traffic = pmc.get("hbm_bytes_per_launch") if same else None
-        packed = kind == 5 or plan.startswith("wavefront16")
+        packed = plan.startswith("wavefront16")
         lane_rate = VALU_LANE_OPS * (2 if packed else 1)
         kcells = cells_per_step / kern_s
-        if wl["ops"]:
+        if kind == 5:
+            # fp32 flops (an FMA counts 2) at the non-packed fp32 VALU rate, 78.6 TFLOPS; packed
+            # v_pk_fma_f32 measured no faster here (profiles/r02_pairhmm_ab.md)
+            peak_cells = 2 * VALU_LANE_OPS / wl["ops"]
+            valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
+                    "unit": "T cells/s", "frac": round(kcells / peak_cells, 4), "ops_per_cell": wl["ops"],
+                    "basis": "SURVEY.md 8(d): 11 fp32 flops per cell (3 FMA = 6, 4 mul, 1 add) at the non-packed "
+                             "fp32 VALU rate 78.6 TFLOPS"}
+        elif wl["ops"]:
             peak_cells = lane_rate / wl["ops"]
             valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
                     "unit": "T cells/s", "frac": round(kcells / peak_cells, 4), "ops_per_cell": wl["ops"],
@@ -627,7 +731,7 @@ def main():
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
         if world == 1 and not args.no_e2e:
-            out["end_to_end"] = end_to_end(eng, kind, data, None if kind == 5 else params, cells_per_step)
+            out["end_to_end"] = end_to_end(eng, kind, data, None if kind in (5, 6) else params, cells_per_step)
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -73,6 +73,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
+#ifndef GX_WF16_TB_INPLACE
+#define GX_WF16_TB_INPLACE 0
+#endif
 #ifndef GX_WF16_TB_WAVES
 #define GX_WF16_TB_WAVES 2   // GLOBAL + traceback kernel
 #endif
@@ -629,10 +632,19 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
             for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
             for (uint32_t s = 0; s < nsteps; s += 4, c += 4) {
+#if GX_WF16_TB_INPLACE
+                // one H array updated in place (each row reads its old H as the next
+                // row's diagonal before writing the new one): R fewer live VGPRs
+                half_step(c, 0, HA, HA);
+                half_step(c + 1, 1, HA, HA);
+                half_step(c + 2, 2, HA, HA);
+                half_step(c + 3, 3, HA, HA);
+#else
                 half_step(c, 0, HA, HB);
                 half_step(c + 1, 1, HB, HA);
                 half_step(c + 2, 2, HA, HB);
                 half_step(c + 3, 3, HB, HA);
+#endif
                 const uint32_t w = s >> 2;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {

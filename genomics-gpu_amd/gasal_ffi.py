@@ -335,6 +335,19 @@ class Engine:
                                           _p(s16)), "nv_score_host")
         return (sc, s16) if int16 else sc
 
+    def nv_score_device_ptrs(self, aligner: "NvAligner", n: int, pat: dict, txt: dict, scores_ptr: int = 0,
+                             scores16_ptr: int = 0, max_pattern_len: int = 0, max_text_len: int = 0, stream: int = 0):
+        """Device-resident nvbio-style scoring: pat/txt = {"words": ptr, "offsets": ptr or 0, "length": int,
+        "bits": int, "big_endian": bool} with device addresses."""
+        mk = lambda d: CNvStrings(d["words"], d.get("offsets") or None, d.get("length", 0), d["bits"],
+                                  int(d.get("big_endian", False)))
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_score_device(self._h, ctypes.byref(ca), ctypes.c_uint32(n), ctypes.byref(mk(pat)),
+                                            ctypes.byref(mk(txt)), ctypes.c_void_p(scores_ptr or None),
+                                            ctypes.c_void_p(scores16_ptr or None), ctypes.c_uint32(max_pattern_len),
+                                            ctypes.c_uint32(max_text_len), ctypes.c_void_p(stream or None)),
+               "nv_score_device")
+
     def pairhmm_device_ptrs(self, ptrs: dict, read_bytes: int, hap_bytes: int, n: int, max_r: int, max_h: int,
                             result_ptr: int, stream: int = 0):
         g = lambda k: ptrs.get(k) or None
