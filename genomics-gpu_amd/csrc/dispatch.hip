@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 
+#include "banded16.hpp"
 #include "engine.hpp"
 #include "generic.hpp"
 #include "pairhmm.hpp"
@@ -169,6 +170,20 @@ static bool int16_safe(const gasalx_params &p, uint32_t mq, uint32_t mt) {
     return std::abs((int64_t)p.gap_open) + L * step < 30000;
 }
 
+// Packed banded kernel (banded16.hpp): stored values B + [0, Hmax] and keys
+// H*8 + 7 + 0x400 inside [0x0400, 0x7BFF]; pads score -b, which needs an N score
+// <= 0.  GASALX_BAND16=0 keeps every pair on the int32 kernel (A/B runs).
+static uint32_t band16_base(const gasalx_params &p) { return 0x400u + (uint32_t)(p.gap_open + p.gap_extend + p.mismatch); }
+static bool band16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
+    const char *env = std::getenv("GASALX_BAND16");
+    if (env && std::atoi(env) == 0) return false;
+    if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
+    if (p.match + p.mismatch > 255 || p.gap_open + p.gap_extend > 4096) return false;
+    if (p.has_n_penalty && p.n_penalty < 0) return false;
+    const int64_t hmax = (int64_t)p.match * std::min(q8, t8);
+    return hmax + band16_base(p) <= 0x7BFF && hmax * 8 + 7 + 0x400 <= 0x7BFF;
+}
+
 Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     Plan pl;
     const uint32_t q8 = pad8(s.max_q), t8 = pad8(s.max_t);
@@ -248,6 +263,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         pl.need_pack = true;
         static const char *names[] = {"?", "global", "semi", "local", "?", "banded", "ksw"};
         pl.name = std::string("generic_") + names[p.algo];
+        if (p.algo == 5 && band16_ok(p, q8, t8)) {
+            pl.band16 = true;
+            pl.name = "banded16_local";
+        }
     } else {
         pl.kind = PLAN_NONE;
         pl.name = "none";
@@ -537,7 +556,42 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                     A.rev = ws.rev.as<uint32_t>();
                 }
                 gen_semi_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
-            } else if (p.algo == 5) gen_banded_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            } else if (p.algo == 5) {
+                if (pl.band16) {
+                    BandArgs D;
+                    std::memset(&D, 0, sizeof(D));
+                    D.qw = A.qw; D.tw = A.tw;
+                    D.qoff = b.q_offsets; D.toff = b.t_offsets; D.qlen = b.q_lens; D.tlen = b.t_lens;
+                    D.score = out.aln_score; D.qend = qend; D.tend = tend;
+                    D.n = n; D.n_lanes = (n + 1) / 2;
+                    D.a = p.match; D.b = p.mismatch; D.oe = p.gap_open + p.gap_extend; D.e = p.gap_extend;
+                    D.kbw = A.kbw; D.nval = A.nval; D.base = band16_base(p);
+                    HIPCHK(ws.misc.reserve(n));
+                    HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
+                    D.todo = ws.misc.as<uint8_t>();
+                    HIPCHK(ws.aux.reserve((size_t)q8 * D.n_lanes * 8 + 64));
+                    D.rows = ws.aux.as<uint2>();
+                    // uneven lengths: pair up slots of equal tile geometry (counting sort)
+                    const uint32_t trw = t8 / 8, nkeys = (q8 / 8) * trw;
+                    const size_t sh = (size_t)(nkeys + 1) * 4;
+                    if (sort_wanted(shape) && n >= 4096 && 2 * sh <= 64 * 1024) {
+                        HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + 2 * sh + 64));
+                        uint32_t *perm = ws.sort_meta.as<uint32_t>(), *klen = perm + n, *hist = klen + n,
+                                 *cursor = hist + nkeys + 1;
+                        band16_key_kernel<<<grid_for(n, 256), 256, 0, st>>>(b.q_lens, b.t_lens, n, trw, klen);
+                        HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+                        rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, hist);
+                        rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nkeys + 1);
+                        rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys,
+                                                                                  cursor, perm);
+                        D.perm = perm;
+                    }
+                    band16_kernel<<<grid_for(D.n_lanes, 256), 256, 0, st>>>(D);
+                    HIPCHK(hipGetLastError());
+                    A.todo = D.todo;
+                }
+                gen_banded_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            }
             else gen_global_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
         }
         HIPCHK(hipGetLastError());

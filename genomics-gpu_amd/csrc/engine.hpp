@@ -52,6 +52,7 @@ struct Plan {
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;
     bool need_pack = false; // generic kernels / reverse-complement need packed words
+    bool band16 = false;    // banded: two pairs per lane in 16-bit halves (banded16.hpp), int32 fallback
     std::string name;
 };
 

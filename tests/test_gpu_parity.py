@@ -341,6 +341,83 @@ def test_banded(engine, k_band):
     check(engine, rand_batch(70 + k_band, 400, 30, 150, 30, 200), algo=G.BANDED, k_band=k_band)
 
 
+def _with_band16(on):
+    if on:
+        os.environ.pop("GASALX_BAND16", None)
+    else:
+        os.environ["GASALX_BAND16"] = "0"
+
+
+def test_banded16_plan():
+    assert G.describe_plan(G.make_params(algo=G.BANDED, k_band=16), 150, 182).startswith("banded16")
+    # N scores > 0 (pads would matter), match + mismatch > 255: the int32 kernel only
+    assert G.describe_plan(G.make_params(algo=G.BANDED, k_band=16, n_penalty=-1), 150, 182) == "generic_banded"
+    assert G.describe_plan(G.make_params(algo=G.BANDED, k_band=16, match=200, mismatch=60), 150, 182) == \
+        "generic_banded"
+
+
+@pytest.mark.parametrize("k_band", [8, 16, 24, 64, 400])
+@pytest.mark.parametrize("scores", [{}, dict(match=2, mismatch=3, gap_open=5, gap_extend=2),
+                                    dict(match=3, mismatch=1, gap_open=1, gap_extend=1, n_penalty=2)])
+def test_banded16_config4_geometry(engine, k_band, scores):
+    # one tile geometry (150 x 182, SURVEY config 4): every lane carries two pairs; an odd
+    # count leaves the last lane one pair
+    check(engine, G.Batch.synth(4, 3001, 0x5EED0004 + k_band), algo=G.BANDED, k_band=k_band, **scores)
+
+
+def test_banded16_pads_differ_per_half(engine):
+    # same (QR, TR) per lane, different ql / tl inside the last words: each half has its
+    # own pad rows and columns
+    rng = np.random.default_rng(91)
+    qs, ts = [], []
+    for _ in range(2000):
+        q = helpers.random_seq(rng, int(rng.integers(145, 153)))
+        t = (helpers.mutate(rng, q) + helpers.random_seq(rng, 60))[:int(rng.integers(177, 185))]
+        qs.append(q); ts.append(t)
+    for k_band in (8, 16, 40):
+        check(engine, G.Batch.from_pairs(qs, ts), algo=G.BANDED, k_band=k_band)
+
+
+@pytest.mark.parametrize("n", [4000, 9001])
+def test_banded16_mixed_geometry(engine, n):
+    # uneven lengths: n >= 4096 pairs slots of equal geometry by a counting sort, smaller
+    # batches decline the second pair of a mismatched lane to the int32 kernel
+    b = rand_batch(95 + n, n, 20, 260, 20, 300)
+    for k_band in (16, 48):
+        check(engine, b, algo=G.BANDED, k_band=k_band)
+
+
+def test_banded16_n_bases_and_iupac(engine):
+    # N / other letters inside a sequence take the int32 kernel (per pair); the rest stay packed
+    rng = np.random.default_rng(97)
+    qs, ts = [], []
+    for i in range(3000):
+        q = bytearray(helpers.random_seq(rng, 150))
+        t = bytearray((helpers.mutate(rng, bytes(q)) + helpers.random_seq(rng, 40))[:182])
+        if i % 7 == 0:
+            q[int(rng.integers(0, 150))] = ord("N")
+        if i % 11 == 0:
+            t[int(rng.integers(0, 182))] = b"NRY"[i % 3]
+        qs.append(bytes(q)); ts.append(bytes(t))
+    b = G.Batch.from_pairs(qs, ts)
+    for kw in ({}, dict(n_penalty=3)):
+        check(engine, b, algo=G.BANDED, k_band=16, **kw)
+
+
+def test_banded16_equals_int32_kernel(engine):
+    # the packed kernel and the reference-shaped int32 kernel on the same batch
+    b = G.Batch.synth(4, 20000, 0x5EED0004)
+    p = G.make_params(algo=G.BANDED, k_band=16)
+    r16 = engine.align_host(b, p)
+    try:
+        _with_band16(False)
+        r32 = engine.align_host(b, p)
+    finally:
+        _with_band16(True)
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(r16[f], r32[f]), f
+
+
 def test_ksw(engine):
     b = rand_batch(80, 500, 10, 150, 10, 150)
     seed = np.random.default_rng(81).integers(0, 60, b.n).astype(np.uint32)
