@@ -11,11 +11,18 @@
 // arithmetic: values stored as value + B inside the positive normal f16 range,
 // where v_pk_maximum3_f16 is an exact 3-way max on both halves
 // (wavefront16.hpp).  Per cell of both pairs: v_perm (substitution byte of the
-// column's table selected by the row's letter), add/sub (diag + s), F and E
-// (one sub + one maximum3 each, floored at 0: exact for H, see below), H
-// (maximum3), H - OE (feeds E of the next column and F of the next row) and
-// the (H, column) key (v_pk_mad_u16): 10 instructions for two cells, against
-// about 16 per cell in the int32 kernel.
+// column's table selected by the row's letter), v_add3 (diag + s, the diagonal
+// taken from the row above's H - OE), F and E (one sub + one maximum3 each,
+// floored at 0: exact for H, see below), H (maximum3), H - OE (feeds E of the
+// next column and F and the diagonal of the next row) and the (H, column) key
+// (v_pk_mad_u16): 9 instructions for two cells, about 12 with the per-row
+// first-maximum update, against about 16 per cell in the int32 kernel.
+//
+// A lane runs strips i and i + 1 in one pass over their rows: strip i's (H, E)
+// at its last column feeds strip i + 1 directly, so the [row][lane] row buffer
+// is read and written once per two strips, and rows entering the band for the
+// first time start from the initial 0 without a load.  The next tile's row
+// buffer entries and query words are loaded one tile ahead.
 //
 // Semantics kept from banded.h: textbook Gotoh on H (F from the H above, E
 // from the H on the left, :94-102); (H, E) of every row carried between strips
@@ -43,6 +50,13 @@
 
 namespace gx {
 
+#ifndef GX_BAND16_WAVES
+#define GX_BAND16_WAVES 3   // waves per SIMD (a few spills; 3.3 % faster than 2 waves at 184 VGPRs)
+#endif
+#ifndef GX_BAND16_SCHED
+#define GX_BAND16_SCHED 0
+#endif
+
 struct BandArgs {
     const uint32_t *qw, *tw;           // packed 4-bit words of the batch
     const uint32_t *qoff, *toff, *qlen, *tlen;
@@ -55,7 +69,87 @@ struct BandArgs {
     uint32_t base;                     // stored value of 0
 };
 
-__global__ __launch_bounds__(256) void band16_kernel(BandArgs A) {
+// exact u16x2 multiply-add in one VOP3P op (the compiler splits a multiply by 8
+// into a shift and an add)
+__device__ __forceinline__ uint32_t band_key(uint32_t h, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 8, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(h), "s"(c));
+    return r;
+}
+
+// [x != y] per 16-bit half as 0x0000 / 0xFFFF, for x >= y per half
+__device__ __forceinline__ uint32_t band_ne_mask(uint32_t x, uint32_t y) {
+    const uint32_t d = pk_subnb(x, y);                                   // no borrow: x >= y per half
+    const uint32_t one = GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, d), GX_AS(pk_u2, 0x00010001u)));
+    return GX_AS(uint32_t, GX_AS(pk_u2, 0u) - GX_AS(pk_u2, one));
+}
+
+// Running first maximum of one strip, both halves: key = H*8 + (7 - column) + 0x400,
+// updated by a row only when the row's H is strictly higher (its B7 = key | 7).
+struct BandBest {
+    uint32_t key, b7, row;
+};
+__device__ __forceinline__ void band_row_max(BandBest &B, const uint32_t (&key)[8], uint32_t rr) {
+    const uint32_t m1 = pk_max3(key[0], key[1], key[2]), m2 = pk_max3(key[3], key[4], key[5]);
+    const uint32_t rk = pk_max3(pk_max3(key[6], key[7], m1), m2, m2);
+    const uint32_t t = pk_max_u16(rk, B.b7);
+    const uint32_t msk = band_ne_mask(t, B.b7);
+    B.key = (B.key & ~msk) | (rk & msk);
+    B.row = (B.row & ~msk) | (rr & msk);
+    B.b7 = t | 0x00070007u;
+}
+
+// One row of 8 columns of one strip for both halves (banded.h:86-107).  The
+// diagonal H(r-1, c-1) is not kept: it is hoe[c-1] + OE of the row above, so
+// tmp = (H(r-1, c-1) - OE) + v + (OE - K) is one v_add3 (C = OE - K per half,
+// exact in 32 bits because every half's result stays inside its window).
+__device__ __forceinline__ void band_row(const uint32_t (&T0)[8], const uint32_t (&T1)[8], uint32_t sel,
+                                         uint32_t (&hoe)[8], uint32_t (&f)[8], uint32_t &hol, uint32_t &left,
+                                         uint32_t &e, uint32_t (&key)[8], const uint32_t (&KC)[8], uint32_t BB,
+                                         uint32_t OE2, uint32_t EXT, uint32_t C) {
+    uint32_t dg = hol;                      // H(r-1, -1) - OE
+    uint32_t loe = pk_subnb(left, OE2);     // H(r, -1) - OE
+    hol = loe;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const uint32_t v = __builtin_amdgcn_perm(T1[m], T0[m], sel);
+        const uint32_t up = hoe[m];         // H(r-1, c) - OE
+        const uint32_t fm = pk_max3(up, pk_subnb(f[m], EXT), BB);
+        const uint32_t tmp = dg + v + C;
+        e = pk_max3(loe, pk_subnb(e, EXT), BB);
+        const uint32_t H = pk_max3(tmp, fm, e);
+        f[m] = fm;
+        left = H;
+        loe = pk_subnb(H, OE2);
+        hoe[m] = loe;
+        dg = up;
+        key[m] = band_key(H, KC[m]);
+    }
+}
+
+// letters as nibbles 0..3 ((code >> 1) & 3: A 0, C 1, T 2, G 3); valid codes 1, 3, 4, 7
+__device__ __forceinline__ bool band_word_ok(uint32_t w, uint32_t nreal) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ok &= (uint32_t)k >= nreal || ((0x9Au >> ((w >> (28 - 4 * k)) & 15u)) & 1u);
+    return ok;
+}
+
+// the 8 substitution tables of one strip for one pair: byte l = score(l, t) + b;
+// pad columns (past tl) score -b in every row
+__device__ __forceinline__ bool band_tables(uint32_t g, uint32_t col0, uint32_t tl, uint32_t match, uint32_t (&T)[8]) {
+    bool ok = true;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+        const uint32_t c = (g >> (28 - 4 * m)) & 15u;
+        const bool real = col0 + m < tl, valid = (0x9Au >> c) & 1u;
+        ok &= !real || valid;
+        T[m] = (real && valid) ? match << (8 * ((c >> 1) & 3u)) : 0u;
+    }
+    return ok;
+}
+
+__global__ __launch_bounds__(256, GX_BAND16_WAVES) void band16_kernel(BandArgs A) {
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= A.n_lanes) return;
     const uint32_t s0 = 2 * lane, s1 = s0 + 1;
@@ -73,100 +167,134 @@ __global__ __launch_bounds__(256) void band16_kernel(BandArgs A) {
     const uint32_t *qwa = A.qw + (A.qoff[pa] >> 3), *qwb = A.qw + (A.qoff[pb] >> 3);
     const uint32_t *twa = A.tw + (A.toff[pa] >> 3), *twb = A.tw + (A.toff[pb] >> 3);
     const uint32_t BB = A.base * 0x10001u, OE2 = (uint32_t)A.oe * 0x10001u, EXT = (uint32_t)A.e * 0x10001u;
-    const uint32_t KK = (uint32_t)A.b * 0x10001u, MATCH = (uint32_t)(A.a + A.b);
+    const uint32_t C = OE2 - (uint32_t)A.b * 0x10001u, MATCH = (uint32_t)(A.a + A.b);
     uint2 *rows = A.rows + lane;
     const size_t rs = A.n_lanes;
-    for (uint32_t r = 0; r < QR * 8; ++r) rows[r * rs] = make_uint2(BB, BB);
     // key = H*8 + (7 - column in strip) + 0x400 = H_stored*8 + KC[m]  (mod 2^16)
     uint32_t KC[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) KC[m] = ((uint32_t)(7 - m + 0x400 - 8 * (int32_t)A.base) & 0xFFFFu) * 0x10001u;
-    bool bad_a = false, bad_b = false;
-    int32_t maxa = 0, maxb = 0, xa = 0, xb = 0, ya = 0, yb = 0;
+    // the query is read once per strip: check its letters once
+    bool ok_a = true, ok_b = true;
+    for (uint32_t j = 0; j < QR; ++j) {
+        ok_a &= band_word_ok(qwa[j], qla - 8 * j);
+        ok_b &= band_word_ok(qwb[j], qlb - 8 * j);
+    }
+    // pad rows of the last query tile: letter nibble 0xC (selector byte 0x0C = 0,
+    // score -b) for the low half, 0x8 (+4 = 0x0C) for the high half
+    const uint32_t kpa = qla - 8 * (QR - 1), kpb = qlb - 8 * (QR - 1);
+    const uint32_t pma = kpa >= 8 ? 0u : (1u << (4 * (8 - kpa))) - 1u;
+    const uint32_t pmb = kpb >= 8 ? 0u : (1u << (4 * (8 - kpb))) - 1u;
+    int32_t gma = 0, gmb = 0, xa = 0, xb = 0, ya = 0, yb = 0;   // FIND_MAX state (banded.h:104, :113)
     const int32_t kother = (int32_t)TR - ((int32_t)QR - A.kbw);   // banded.h:35
-    for (int32_t i = 0; i < (int32_t)TR; ++i) {
-        // the strip's 8 substitution tables per pair: byte l = score(l, t) + b
-        uint32_t T0[8], T1[8];
-        const uint32_t ga = twa[i], gb = twb[i];
+    // strips i and i + 1 in one pass over their rows: strip i's (H, E) at its last
+    // column feeds strip i + 1 directly, so the row buffer is read and written once
+    // per two strips
+    for (int32_t i = 0; i < (int32_t)TR; i += 2) {
+        const bool hasB = i + 1 < (int32_t)TR;
+        uint32_t TA0[8], TA1[8], TB0[8], TB1[8];
+        ok_a &= band_tables(twa[i], 8 * i, tla, MATCH, TA0);
+        ok_b &= band_tables(twb[i], 8 * i, tlb, MATCH, TA1);
+        if (hasB) {
+            ok_a &= band_tables(twa[i + 1], 8 * i + 8, tla, MATCH, TB0);
+            ok_b &= band_tables(twb[i + 1], 8 * i + 8, tlb, MATCH, TB1);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) TB0[m] = TB1[m] = 0u;
+        }
+        uint32_t hoeA[8], fA[8], hoeB[8], fB[8], holA = BB - OE2, holB = BB - OE2;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const uint32_t col = (uint32_t)i * 8 + m;
-            const uint32_t la = letter_of((ga >> (28 - 4 * m)) & 15u, A.nval);
-            const uint32_t lb = letter_of((gb >> (28 - 4 * m)) & 15u, A.nval);
-            const bool ra = col < tla, rb = col < tlb;
-            bad_a |= ra && la > 3;
-            bad_b |= rb && lb > 3;
-            T0[m] = (ra && la < 4) ? MATCH << (8 * la) : 0u;
-            T1[m] = (rb && lb < 4) ? MATCH << (8 * lb) : 0u;
+            hoeA[m] = hoeB[m] = BB - OE2;
+            fA[m] = fB[m] = BB;
         }
-        uint32_t hoe[8], f[8], p[8];   // row above: H - OE, F, and diag H(r-1, c-1)
-#pragma unroll
-        for (int m = 0; m < 8; ++m) { hoe[m] = BB - OE2; f[m] = BB; p[m] = BB; }
-        const int32_t j0 = max(0, i - kother + 1), j1 = min(A.kbw + i, (int32_t)QR);   // banded.h:73-75
-        // the tile's 8 row-buffer entries and query words, loaded one tile ahead
+        const int32_t j0A = max(0, i - kother + 1), j1A = min(A.kbw + i, (int32_t)QR);   // banded.h:73-75
+        const int32_t j0B = max(0, i + 1 - kother + 1), j1B = hasB ? min(A.kbw + i + 1, (int32_t)QR) : j1A;
+        // row tiles >= fresh were never written (j1 only grows): their (H, E) is the
+        // initial 0 (banded.h:61-63) without a load
+        const int32_t fresh = i == 0 ? 0 : min(A.kbw + i - 1, (int32_t)QR);
+        BandBest bA = {0x04070407u, 0x04070407u, 0u}, bB = bA;
+        // one tile of 8 rows: strip i (DA), strip i + 1 (DB), or both; three loops so
+        // that no row branches (the register rotation of p / left stays free)
+        // row-buffer entries and query words of the tile, loaded one tile ahead
+        // (tiles >= fresh start at the initial 0 without a load)
         uint2 cur[8];
-        uint32_t wa = 0, wb = 0;
-        if (j0 < j1) {
-            wa = qwa[j0]; wb = qwb[j0];
+        uint32_t cwa = 0, cwb = 0;
+        auto load = [&](int32_t j, uint2 (&dst)[8], uint32_t &wa, uint32_t &wb) {
+            if (j < fresh) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = rows[((uint32_t)j0 * 8 + k) * rs];
-        }
-        for (int32_t j = j0; j < j1; ++j) {
+                for (int k = 0; k < 8; ++k) dst[k] = rows[((uint32_t)j * 8 + k) * rs];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) dst[k] = make_uint2(BB, BB);
+            }
+            if (j < (int32_t)QR) { wa = qwa[j]; wb = qwb[j]; }
+        };
+        auto tile = [&](int32_t j, auto DA, auto DB) {
+            constexpr bool doA = decltype(DA)::value, doB = decltype(DB)::value;
             uint2 nxt[8];
             uint32_t nwa = 0, nwb = 0;
-            if (j + 1 < j1) {
-                nwa = qwa[j + 1]; nwb = qwb[j + 1];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) nxt[k] = rows[((uint32_t)j * 8 + 8 + k) * rs];
-            }
+            load(j + 1, nxt, nwa, nwb);
+            uint32_t la = (cwa >> 1) & 0x33333333u, lb = (cwb >> 1) & 0x33333333u;
+            if (j == (int32_t)QR - 1) { la = (la & ~pma) | (0xCCCCCCCCu & pma); lb = (lb & ~pmb) | (0x88888888u & pmb); }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const uint32_t r = (uint32_t)j * 8 + k;
-                const uint32_t la = letter_of((wa >> (28 - 4 * k)) & 15u, A.nval);
-                const uint32_t lb = letter_of((wb >> (28 - 4 * k)) & 15u, A.nval);
-                const bool ra = r < qla, rb = r < qlb;
-                bad_a |= ra && la > 3;
-                bad_b |= rb && lb > 3;
-                const uint32_t sa = (ra && la < 4) ? la : 0x0Cu, sb = (rb && lb < 4) ? lb + 4 : 0x0Cu;
-                const uint32_t sel = sa | 0x0C00u | (sb << 16) | 0x0C000000u;
-                uint32_t left = cur[k].x, e = cur[k].y;        // H, E of the row at the previous strip's last column
-                uint32_t loe = left - OE2;
-                uint32_t key[8];
-#pragma unroll
-                for (int m = 0; m < 8; ++m) {
-                    const uint32_t v = __builtin_amdgcn_perm(T1[m], T0[m], sel);
-                    const uint32_t fm = pk_max3(hoe[m], pk_subnb(f[m], EXT), BB);
-                    const uint32_t tmp = pk_subnb(pk_addnc(p[m], v), KK);
-                    e = pk_max3(loe, pk_subnb(e, EXT), BB);
-                    const uint32_t H = pk_max3(tmp, fm, e);
-                    f[m] = fm;
-                    p[m] = left;
-                    left = H;
-                    loe = pk_subnb(H, OE2);
-                    hoe[m] = loe;
-                    key[m] = pk_mad_u16(H, 0x00080008u, KC[m]);
+                const uint32_t rr = ((uint32_t)j * 8 + k) * 0x10001u;
+                const uint32_t sel = (((la >> (28 - 4 * k)) & 15u) | (((lb >> (28 - 4 * k)) & 15u) << 16)) + 0x0C040C00u;
+                uint32_t left = cur[k].x, e = cur[k].y, key[8];
+                if (doA) {
+                    band_row(TA0, TA1, sel, hoeA, fA, holA, left, e, key, KC, BB, OE2, EXT, C);
+                    band_row_max(bA, key, rr);
+#if GX_BAND16_SCHED
+                    __builtin_amdgcn_sched_barrier(0);   // keep strip i and i + 1 rows apart: registers
+#endif
                 }
-                rows[r * rs] = make_uint2(left, e);
-                const uint32_t m1 = pk_max3(key[0], key[1], key[2]), m2 = pk_max3(key[3], key[4], key[5]);
-                const uint32_t rk = pk_max3(pk_max3(key[6], key[7], m1), m2, m2);
-                const int32_t ka = (int32_t)(rk & 0xFFFFu) - 0x400, kb = (int32_t)(rk >> 16) - 0x400;
-                if ((ka >> 3) > maxa) { maxa = ka >> 3; ya = i * 8 + 7 - (ka & 7); xa = (int32_t)r; }
-                if ((kb >> 3) > maxb) { maxb = kb >> 3; yb = i * 8 + 7 - (kb & 7); xb = (int32_t)r; }
+                if (doB) {
+                    band_row(TB0, TB1, sel, hoeB, fB, holB, left, e, key, KC, BB, OE2, EXT, C);
+                    band_row_max(bB, key, rr);
+                    rows[((uint32_t)j * 8 + k) * rs] = make_uint2(left, e);
+#if GX_BAND16_SCHED
+                    __builtin_amdgcn_sched_barrier(0);
+#endif
+                }
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
-            wa = nwa; wb = nwb;
+            cwa = nwa; cwb = nwb;
+        };
+        // the tiles a pass visits are contiguous from here (j0B <= j0A + 1 <= j1A when
+        // strip i's band is not empty)
+        load(j0A < j1A || !hasB ? j0A : j0B, cur, cwa, cwb);
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        if (!hasB) {
+            for (int32_t j = j0A; j < j1A; ++j) tile(j, T_{}, F_{});
+        } else {
+            // tiles of strip i: [j0A, j1A), of strip i + 1: [j0B, j1B), j0B >= j0A, j1B >= j1A
+            for (int32_t j = j0A; j < min(j1A, j0B); ++j) tile(j, T_{}, F_{});   // above strip i + 1's band
+            for (int32_t j = j0B; j < j1A; ++j) tile(j, T_{}, T_{});
+            for (int32_t j = max(j0B, j1A); j < j1B; ++j) tile(j, F_{}, T_{});   // below strip i's band
+        }
+        // strip-major order: strip i's first maximum, then strip i + 1's, each only
+        // when strictly above the maximum so far
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const BandBest &b = s ? bB : bA;
+            const int32_t col0 = 8 * (i + s) + 7;
+            const int32_t ka = (int32_t)(b.key & 0xFFFFu) - 0x400, kb = (int32_t)(b.key >> 16) - 0x400;
+            if ((ka >> 3) > gma) { gma = ka >> 3; ya = col0 - (ka & 7); xa = (int32_t)(b.row & 0xFFFFu); }
+            if ((kb >> 3) > gmb) { gmb = kb >> 3; yb = col0 - (kb & 7); xb = (int32_t)(b.row >> 16); }
         }
     }
-    A.score[pa] = maxa;
+    A.score[pa] = gma;
     if (A.qend) A.qend[pa] = xa;
     if (A.tend) A.tend[pa] = ya;
-    if (bad_a) A.todo[pa] = 1;
+    if (!ok_a) A.todo[pa] = 1;
     if (two) {
-        A.score[pb] = maxb;
+        A.score[pb] = gmb;
         if (A.qend) A.qend[pb] = xb;
         if (A.tend) A.tend[pb] = yb;
-        if (bad_b) A.todo[pb] = 1;
+        if (!ok_b) A.todo[pb] = 1;
     }
 }
 
