@@ -259,6 +259,22 @@ def cells_of(batch):
     return int(np.sum(batch.q_lens.astype(np.int64) * batch.t_lens.astype(np.int64)))
 
 
+def band_cells_of(batch, k_band):
+    """Cells the banded-tiled kernel computes: 64 per 8x8 tile of the band, strip i
+    covering query tiles [max(0, i - kother + 1), min(k_band/8 + i, QR)) with
+    kother = TR - (QR - k_band/8) (banded.h:35, :73-75)."""
+    kbw = k_band >> 3
+    qr = (batch.q_lens.astype(np.int64) + 7) // 8
+    tr = (batch.t_lens.astype(np.int64) + 7) // 8
+    total = 0
+    for (a, b), cnt in zip(*np.unique(np.stack([qr, tr], 1), axis=0, return_counts=True)):
+        ko = b - (a - kbw)
+        a, b, ko = int(a), int(b), int(ko)
+        tiles = sum(max(0, min(kbw + i, a) - max(0, i - ko + 1)) for i in range(b))
+        total += int(cnt) * 64 * tiles
+    return total
+
+
 def single_core_rate(O, kind, data, pkw, budget_s):
     """The oracle on 1 thread over a prefix of the rank-0 shard, bounded by budget_s."""
     chunk = 256 if kind in (5, 6) else 4096
@@ -398,6 +414,8 @@ def dtype_label(plan, kind):
         return "int32"
     if plan.startswith("wavefront16"):
         return "int16x2 packed (exact value window), int32 fallback per declined block"
+    if plan.startswith("banded16"):
+        return "int16x2 packed (two pairs per lane, exact value window), int32 fallback per declined pair"
     if plan.startswith("wavefront_"):
         return "int32"
     return "int32 (int16 row buffer, as the reference)"
@@ -693,9 +711,18 @@ def main():
                               f"no per-cell running max) at {'packed 2x16-bit / 2xfp32' if packed else 'int32'} "
                               f"VALU lane rate {lane_rate / 1e12:.1f} T ops/s")}
         else:
-            valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": None, "unit": "T cells/s",
-                    "frac": None, "basis": "none: cells are counted over the full rectangle, the banded kernel "
-                                           "computes only the band (banded.h:35,83-85)"}
+            # banded: GCUPS counts the full rectangle (the metric's cells); the kernel
+            # computes the tiles of the band only, so its roofline is over those
+            bcells = band_cells_of(data, pkw.get("k_band", 0))
+            bk = bcells / kern_s
+            rate = VALU_LANE_OPS * (2 if plan.startswith("banded16") else 1)
+            peak_cells = rate / 12
+            valu = {"bound": "valu", "achieved": round(bk / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
+                    "unit": "T cells/s (cells of the band)", "frac": round(bk / peak_cells, 4), "ops_per_cell": 12,
+                    "band_cells_per_step": bcells, "band_fraction": round(bcells / cells_per_step, 4),
+                    "basis": "SURVEY.md 8(d) 12 algorithmic ops per local cell over the cells of the band "
+                             "(banded.h:35,73-75) at the " + ("packed 2x16-bit" if rate > VALU_LANE_OPS else "int32") +
+                             f" VALU lane rate {rate / 1e12:.1f} T ops/s"}
         if same and pmc.get("valu_insts_per_launch"):
             valu["issue"] = {"valu_wave_instr_per_launch": pmc["valu_insts_per_launch"],
                              "cycles_per_valu_instr_per_simd":

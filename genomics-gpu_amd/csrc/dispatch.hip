@@ -542,9 +542,8 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         const size_t rows_elems = (size_t)A.rows_cap * n;
         if (p.algo == 6) {
             const size_t ke = (size_t)(shape.max_q + 8) * n;
-            HIPCHK(ws.rows_h.reserve(ke * 4));
-            HIPCHK(ws.rows_e.reserve(ke * 4));
-            gen_ksw_kernel<<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.as<int32_t>(), ws.rows_e.as<int32_t>());
+            HIPCHK(ws.rows_h.reserve(ke * 8));
+            gen_ksw_kernel<<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.as<int2>());
         } else {
             HIPCHK(ws.rows_h.reserve(rows_elems * 2));
             HIPCHK(ws.rows_e.reserve(rows_elems * 2));

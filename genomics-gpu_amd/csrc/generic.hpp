@@ -401,72 +401,101 @@ __global__ __launch_bounds__(256) void gen_banded_kernel(GenArgs A) {
 }
 
 // ------------------------------------------------------------------ KSW ----
-// eh[] of the reference (ksw_kernel_template.h:69) = rowH (h) and rowE (e) as
-// int32 pairs in the rows scratch viewed as int32.
-__global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int32_t *ehh, int32_t *ehe) {
+// eh[] of the reference (ksw_kernel_template.h:69) as (h, e) int32 pairs in one
+// 8-byte entry, [column][pair]: one load and one store per cell.  The row's
+// beg/end trimming scans (:181-186) are tracked while the row is computed (first
+// and last stored entry that is not (0, 0)) instead of re-reading the row.
+// Rows are iterated in lockstep by the wave (a lane that the reference would
+// `break` out of a tile just sits the rows out), so that every row's column
+// loop can start at the wave's smallest beg — the lanes then touch the same
+// column, and the [column][pair] entries stay coalesced.
+__device__ __forceinline__ int ksw_wave_min(int v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = min(v, __shfl_xor(v, m));
+    return v;
+}
+__device__ __forceinline__ int ksw_wave_max(int v) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v = max(v, __shfl_xor(v, m));
+    return v;
+}
+
+__global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int2 *ehp) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= A.n) return;
-    const uint32_t qlen = A.qlen[tid], tlen = A.tlen[tid];
-    const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
-    const uint32_t *tw = A.tw + (A.toff[tid] >> 3);
-    const uint32_t QR = (qlen >> 3) + 1, TR = (tlen >> 3) + 1;       // Q16
-    const uint32_t h0 = A.seed ? A.seed[tid] : 0u;
+    const bool live = tid < A.n;   // lanes past n run the wave's row loop without work
+    const uint32_t qlen = live ? A.qlen[tid] : 0u, tlen = live ? A.tlen[tid] : 0u;
+    const uint32_t *qw = A.qw + (live ? A.qoff[tid] >> 3 : 0u);
+    const uint32_t *tw = A.tw + (live ? A.toff[tid] >> 3 : 0u);
+    const uint32_t h0 = (live && A.seed) ? A.seed[tid] : 0u;
     const int o_del = A.o, o_ins = A.o, e_del = A.e, e_ins = A.e;
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
-#define EH(j) ehh[(size_t)(j) * A.n + tid]
-#define EE(j) ehe[(size_t)(j) * A.n + tid]
-    for (uint32_t j = 0; j < qlen + 2; j++) { EH(j) = 0; EE(j) = 0; }
-    EH(0) = (int32_t)h0;
-    EH(1) = (h0 > (uint32_t)oe_ins) ? (int32_t)(h0 - (uint32_t)oe_ins) : 0;
-    for (int j = 2; j <= (int)qlen && EH(j - 1) > e_ins; ++j) EH(j) = EH(j - 1) - e_ins;
-    int max_ = (int32_t)h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1;
-    int beg = 0, end = (int)qlen, j = 0;
-    for (uint32_t tt = 0; tt < TR; tt++) {
-        const uint32_t gpac = tw[tt];
-        for (uint32_t tb = 0; tb < 8; tb++) {
-            const int i = (int)(tt * 8 + tb);
-            if (i >= (int)tlen) break;
-            const uint32_t gbase = (gpac >> (32 - (tb + 1) * 4)) & 0x0F;
-            int t, f = 0, h1, m = 0, mj = -1;
-            if (beg == 0) {
-                h1 = (int32_t)(h0 - (uint32_t)(o_del + e_del * (i + 1)));
-                if (h1 < 0) h1 = 0;
-            } else h1 = 0;
-            for (uint32_t qt = 0; qt < QR; qt++) {
-                const uint32_t rpac = qw[qt];
-                for (uint32_t qb = 0; qb < 8; qb++) {
-                    j = (int)(qt * 8 + qb);
-                    if (j < beg) continue;
-                    if (j >= end) break;
-                    const uint32_t rbase = (rpac >> (32 - (qb + 1) * 4)) & 0x0F;
-                    int h, M = EH(j), e = EE(j);
-                    EH(j) = h1;
-                    M = M ? M + g_sub_local(A, rbase, gbase) : 0;
-                    h = M > e ? M : e;
-                    h = h > f ? h : f;
-                    h1 = h;
-                    mj = m > h ? mj : j;
-                    m = m > h ? m : h;
-                    t = M - oe_del; t = t > 0 ? t : 0;
-                    e -= e_del; e = e > t ? e : t;
-                    EE(j) = e;
-                    t = M - oe_ins; t = t > 0 ? t : 0;
-                    f -= e_ins; f = f > t ? f : t;
-                }
-            }
-            EH(end) = h1; EE(end) = 0;
-            if (j == (int)qlen) {
-                max_ie = gscore > h1 ? max_ie : i;
-                gscore = gscore > h1 ? gscore : h1;
-            }
-            if (m == 0) break;
-            if (m > max_) { max_ = m; max_i = i; max_j = mj; }
-            for (j = beg; (j < end) && EH(j) == 0 && EE(j) == 0; ++j) ;
-            beg = j;
-            for (j = end; (j >= beg) && EH(j) == 0 && EE(j) == 0; --j) ;
-            end = j + 2 < (int)qlen ? j + 2 : (int)qlen;
-        }
+#define EHP(j) ehp[(size_t)(j) * A.n + tid]
+    if (live) {
+        for (uint32_t j = 0; j < qlen + 2; j++) EHP(j) = make_int2(0, 0);
+        int h = (int32_t)h0;       // the first row (:72-76)
+        EHP(0) = make_int2(h, 0);
+        h = (h0 > (uint32_t)oe_ins) ? (int32_t)(h0 - (uint32_t)oe_ins) : 0;
+        EHP(1) = make_int2(h, 0);
+        for (int j = 2; j <= (int)qlen && h > e_ins; ++j) { h -= e_ins; EHP(j) = make_int2(h, 0); }
     }
+    int max_ = (int32_t)h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1;
+    int beg = 0, end = (int)qlen;
+    // target rows in tiles of 8 (TR = tlen/8 + 1 words, Q16); `m == 0` skips the rest
+    // of the tile (:165-166), a row past tlen ends it (:101-102)
+    const int imax = ksw_wave_max((int)tlen);
+    bool skip = false;
+    uint32_t gpac = 0;
+    for (int i = 0; i < imax; ++i) {
+        if ((i & 7) == 0) {
+            skip = false;
+            if (i < (int)tlen) gpac = tw[i >> 3];
+        }
+        const bool act = i < (int)tlen && !skip;
+        const int jlo = ksw_wave_min(act ? beg : 0x7FFFFFFF);
+        if (!act) continue;
+        const uint32_t gbase = (gpac >> (28 - 4 * (i & 7))) & 0x0F;
+        int t, f = 0, h1, m = 0, mj = -1;
+        if (beg == 0) {
+            h1 = (int32_t)(h0 - (uint32_t)(o_del + e_del * (i + 1)));
+            if (h1 < 0) h1 = 0;
+        } else h1 = 0;
+        int first = end, last = beg - 1;   // stored entries other than (0, 0) in [beg, end]
+        uint32_t rpac = qw[(uint32_t)jlo >> 3];
+        for (int j = jlo; j < end; ++j) {
+            if ((j & 7) == 0) rpac = qw[(uint32_t)j >> 3];
+            if (j < beg) continue;
+            const uint32_t rbase = (rpac >> (28 - 4 * (j & 7))) & 0x0F;
+            const int2 v = EHP(j);
+            int h, M = v.x, e = v.y;
+            const int hs = h1;           // H(i, j-1), stored for the next row
+            M = M ? M + g_sub_local(A, rbase, gbase) : 0;
+            h = M > e ? M : e;
+            h = h > f ? h : f;
+            h1 = h;
+            mj = m > h ? mj : j;
+            m = m > h ? m : h;
+            t = M - oe_del; t = t > 0 ? t : 0;
+            e -= e_del; e = e > t ? e : t;
+            EHP(j) = make_int2(hs, e);
+            if ((hs | e) != 0) { first = min(first, j); last = j; }   // h, e >= 0
+            t = M - oe_ins; t = t > 0 ? t : 0;
+            f -= e_ins; f = f > t ? f : t;
+        }
+        EHP(end) = make_int2(h1, 0);
+        if (h1 != 0) { first = min(first, end); last = end; }
+        // the reference's column index after its loops is qlen exactly when the
+        // row ended at qlen or qlen is a multiple of 8 (Q16's extra word)
+        if (end == (int)qlen || (qlen & 7u) == 0) {
+            max_ie = gscore > h1 ? max_ie : i;
+            gscore = gscore > h1 ? gscore : h1;
+        }
+        if (m == 0) { skip = true; continue; }
+        if (m > max_) { max_ = m; max_i = i; max_j = mj; }
+        beg = min(first, end);                                  // :181-183
+        if (last < beg) last = beg - 1;                         // the backward scan stops at beg
+        end = last + 2 < (int)qlen ? last + 2 : (int)qlen;      // :184-186
+    }
+    if (!live) return;
     if (gscore <= 0 || gscore <= max_ - 5) {
         A.score[tid] = max_;
         if (A.qend) A.qend[tid] = max_j + 1;
@@ -476,8 +505,7 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int32_t *ehh, i
         if (A.qend) A.qend[tid] = (int32_t)qlen;
         if (A.tend) A.tend[tid] = max_ie + 1;
     }
-#undef EH
-#undef EE
+#undef EHP
 }
 
 // ------------------------------------------------------------- traceback ----

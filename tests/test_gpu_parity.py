@@ -424,6 +424,19 @@ def test_ksw(engine):
     check(engine, b, seed=seed, algo=G.KSW)
 
 
+@pytest.mark.parametrize("lens,seeds", [((1, 40), (0, 5)), ((8, 8), (0, 30)), ((64, 64), (0, 100)),
+                                        ((100, 260), (0, 200)), ((150, 150), (10, 11))])
+def test_ksw_trimming(engine, lens, seeds):
+    # beg/end trimming (ksw_kernel_template.h:181-186) tracked in registers: rows that die
+    # early (small seeds), query lengths that are multiples of 8 (the gscore test after the
+    # column loop, Q16), unrelated pairs (m == 0 ends a tile early)
+    rng = np.random.default_rng(lens[0] * 7 + seeds[1])
+    b = rand_batch(int(rng.integers(1 << 16)), 1500, *lens, *lens, related=0.6)
+    seed = rng.integers(*seeds, b.n).astype(np.uint32)
+    check(engine, b, seed=seed, algo=G.KSW)
+    check(engine, b, seed=seed, algo=G.KSW, match=2, mismatch=3, gap_open=5, gap_extend=2)
+
+
 # ------------------------------------------------ reverse / complement ----
 @pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL, G.SEMI_GLOBAL])
 def test_reverse_complement_ops(engine, algo):
