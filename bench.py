@@ -512,7 +512,7 @@ def main():
         result = gather.buf if gather else torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         pat = {"words": dpw.data_ptr(), "offsets": dpo.data_ptr(), "bits": 4, "big_endian": True}
         txt = {"words": dtw.data_ptr(), "offsets": 0, "length": NV_REF_LEN, "bits": 2, "big_endian": False}
-        plan = "nvbio gotoh semi-global, lane groups of 16 x 16 rows (batched.hip)"
+        plan = G.nv_describe_plan(al, rl, hl)
 
         def align():
             eng.nv_score_device_ptrs(al, n, pat, txt, result.data_ptr(), 0, rl, hl, stream.cuda_stream)

@@ -16,14 +16,16 @@ namespace gx {
 namespace {
 
 struct NvShape { int G, R; };
-constexpr NvShape kNvShapes[] = {{8, 8}, {8, 16}, {16, 16}, {32, 16}, {64, 16}};
+// the smallest G*R >= the longest pattern: 150-bp reads take (8, 19), 152 rows
+constexpr NvShape kNvShapes[] = {{8, 8}, {8, 12}, {8, 16}, {8, 19}, {8, 24}, {16, 16}, {16, 20}, {32, 16}, {64, 16}};
 
 using NvFn = void (*)(NvArgs);
 
 template <int ALN, int TYPE, bool MASK>
 NvFn nv_pick(int G, int R) {
 #define GX_CASE(g, r) if (G == g && R == r) return &nv_kernel<ALN, TYPE, g, r, MASK>;
-    GX_CASE(8, 8) GX_CASE(8, 16) GX_CASE(16, 16) GX_CASE(32, 16) GX_CASE(64, 16)
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 24) GX_CASE(16, 16) GX_CASE(16, 20)
+    GX_CASE(32, 16) GX_CASE(64, 16)
 #undef GX_CASE
     return nullptr;
 }
@@ -39,7 +41,30 @@ NvFn nv_lookup(bool gotoh, int type, bool mask, int G, int R) {
     return mask ? nv_pick<NV_SW, NV_LOCAL, true>(G, R) : nv_pick<NV_SW, NV_LOCAL, false>(G, R);
 }
 
+// the lane-group shape for patterns up to max_p: the smallest G*R that covers them
+// whose text slots fit in LDS (one shared slot, or one per pair)
+const NvShape *nv_shape(uint32_t max_p, uint32_t stride, bool per_pair_text, size_t *lds_out) {
+    for (const NvShape &sh : kNvShapes) {
+        if ((uint32_t)(sh.G * sh.R) < max_p) continue;
+        const size_t lds = per_pair_text ? (size_t)4 * (64 / sh.G) * stride * 2 : (size_t)stride * 2;
+        if (lds > 160 * 1024) continue;
+        *lds_out = lds;
+        return &sh;
+    }
+    return nullptr;
+}
+
 }  // namespace
+
+std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text) {
+    static const char *an[] = {"ed", "sw", "gotoh"}, *tn[] = {"global", "local", "semi"};
+    if (al.aligner < 0 || al.aligner > 2 || al.type < 0 || al.type > 2) return "none";
+    size_t lds = 0;
+    const NvShape *sh = nv_shape(max_p, (std::max<uint32_t>(max_t, 1) + 7u) & ~7u, per_pair_text, &lds);
+    if (!sh) return "none";
+    return std::string("nvbio_") + an[al.aligner] + "_" + tn[al.type] + (per_pair_text ? "" : "_shared") + "_G" +
+           std::to_string(sh->G) + "R" + std::to_string(sh->R);
+}
 
 int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
                     const gasalx_nv_strings &txt, int32_t *scores, int16_t *scores16, uint32_t max_p, uint32_t max_t,
@@ -69,18 +94,16 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
     const bool mask = al.type == NV_LOCAL &&
                       (A.mismatch > 0 || (gotoh ? (A.go > 0 || A.ge > 0) : (A.del > 0 || A.ins > 0)));
     const uint32_t stride = (std::max<uint32_t>(max_t, 1) + 7u) & ~7u;
-    for (const NvShape &sh : kNvShapes) {
-        if ((uint32_t)(sh.G * sh.R) < max_p) continue;
-        const size_t lds = txt.offsets ? (size_t)4 * (64 / sh.G) * stride * 2 : (size_t)stride * 2;
-        if (lds > 160 * 1024) continue;
+    size_t lds = 0;
+    const NvShape *sh = nv_shape(max_p, stride, txt.offsets != nullptr, &lds);
+    NvFn fn = sh ? nv_lookup(gotoh, al.type, mask, sh->G, sh->R) : nullptr;
+    if (fn) {
         A.lds_stride = stride;
-        NvFn fn = nv_lookup(gotoh, al.type, mask, sh.G, sh.R);
-        if (!fn) break;
         if (lds > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
         }
-        const uint32_t per_block = 4 * (64 / sh.G);
+        const uint32_t per_block = 4 * (64 / sh->G);
         hipLaunchKernelGGL(fn, dim3((n + per_block - 1) / per_block), dim3(256), lds, st, A);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }

@@ -32,7 +32,7 @@ EXPORTS = (
     "gasalx_pairhmm_device", "gasalx_pairhmm_host", "gasalx_pairhmm_params", "gasalx_synth_sizes",
     "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
     "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
-    "gasalx_nv_score_device", "gasalx_nv_score_host",
+    "gasalx_nv_score_device", "gasalx_nv_score_host", "gasalx_nv_describe_plan",
 )
 
 # nvbio front-end (gasalx_nv_*): aligners and AlignmentType (nvbio/alignment/alignment_base.h:54)
@@ -367,6 +367,14 @@ def synth_spec(kind: int):
 def describe_plan(params: Params, max_q: int, max_t: int) -> str:
     buf = ctypes.create_string_buffer(128)
     _check(lib().gasalx_describe_plan(ctypes.byref(params), max_q, max_t, buf, 128), "describe_plan")
+    return buf.value.decode()
+
+
+def nv_describe_plan(aligner: "NvAligner", max_p: int, max_t: int, per_pair_texts: bool = False) -> str:
+    buf = ctypes.create_string_buffer(128)
+    al = aligner.cstruct()
+    _check(lib().gasalx_nv_describe_plan(ctypes.byref(al), max_p, max_t, int(per_pair_texts), buf, 128),
+           "nv_describe_plan")
     return buf.value.decode()
 
 

@@ -80,15 +80,17 @@ def test_packings(engine, bits, big):
         _check(engine, _al(ALIGNERS[0], type_), G.PackedSet.pack(pats, bits, big), G.PackedSet.pack(texts, bits, big))
 
 
-@pytest.mark.parametrize("m", [8, 64, 65, 128, 129, 256, 257, 512, 513, 1024])
+@pytest.mark.parametrize("m", [8, 64, 65, 96, 97, 128, 129, 152, 153, 192, 193, 256, 257, 320, 321, 512, 513, 1024])
 def test_pattern_lengths_every_shape(engine, m):
-    # lane-group shapes (8,8) (8,16) (16,16) (32,16) (64,16) of batched.hip, at their edges
+    # lane-group shapes (8,8) (8,12) (8,16) (8,19) (8,24) (16,16) (16,20) (32,16) (64,16) of
+    # batched.hip, at their edges
     rng = np.random.default_rng(m)
     text = list(rng.integers(0, 4, 2200))
     pats = [np.array(_related(rng, text, m - int(rng.integers(0, 3))), np.uint32) for _ in range(96)]
     T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
     for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
         _check(engine, _al(ALIGNERS[0], type_), G.PackedSet.pack(pats), T)
+    assert G.nv_describe_plan(ALIGNERS[0], m, 2200).startswith("nvbio_gotoh_global_shared_G")
 
 
 def test_empty_and_positive_scores(engine):
