@@ -411,7 +411,8 @@ def dtype_label(plan, kind):
     if kind == 5:
         return "fp32"
     if kind == 6:
-        return "int32"
+        return "int16x2 packed (two pairs per lane group, exact value window)" if plan.startswith("nvbio16") \
+            else "int32"
     if plan.startswith("wavefront16"):
         return "int16x2 packed (exact value window), int32 fallback per declined block"
     if plan.startswith("banded16"):
@@ -692,7 +693,7 @@ def main():
                 pmc = None
         same = pmc is not None and pmc.get("pairs_per_launch") == n
         traffic = pmc.get("hbm_bytes_per_launch") if same else None
-        packed = plan.startswith("wavefront16")
+        packed = plan.startswith(("wavefront16", "nvbio16"))
         lane_rate = VALU_LANE_OPS * (2 if packed else 1)
         kcells = cells_per_step / kern_s
         if kind == 5:

@@ -10,6 +10,7 @@
 
 #include "engine.hpp"
 #include "nvbio.hpp"
+#include "nvbio16.hpp"
 
 namespace gx {
 
@@ -28,6 +29,46 @@ NvFn nv_pick(int G, int R) {
     GX_CASE(32, 16) GX_CASE(64, 16)
 #undef GX_CASE
     return nullptr;
+}
+
+using Nv16Fn = void (*)(Nv16Args);
+template <int ALN, int TYPE>
+Nv16Fn nv16_pick(int G, int R) {
+#define GX_CASE(g, r) if (G == g && R == r) return &nv16_kernel<ALN, TYPE, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 24) GX_CASE(16, 16) GX_CASE(16, 20)
+    GX_CASE(32, 16) GX_CASE(64, 16)
+#undef GX_CASE
+    return nullptr;
+}
+template <int ALN>
+Nv16Fn nv16_lookup_t(int type, int G, int R) {
+    return type == NV_GLOBAL ? nv16_pick<ALN, NV_GLOBAL>(G, R)
+         : type == NV_SEMI ? nv16_pick<ALN, NV_SEMI>(G, R) : nv16_pick<ALN, NV_LOCAL>(G, R);
+}
+Nv16Fn nv16_lookup(int aln, int type, int G, int R) {
+    return aln == NV_GOTOH ? nv16_lookup_t<NV_GOTOH>(type, G, R) : nv16_lookup_t<NV_SW>(type, G, R);
+}
+
+// The packed kernel (nvbio16.hpp): one shared 2-bit text, gaps and (LOCAL) mismatches
+// <= 0, match - mismatch in a byte, and every value (bounded by (M + N + 2) * the
+// largest score magnitude) inside the 16-bit f16 window.  GASALX_NV16=0: int32 only.
+bool nv16_ok(int aligner, int type, int32_t match, int32_t mismatch, int32_t go, int32_t ge, int32_t del, int32_t ins,
+             bool shared_text, uint32_t text_bits, uint32_t max_p, uint32_t max_t, uint32_t *base) {
+    const char *env = std::getenv("GASALX_NV16");
+    if (env && std::atoi(env) == 0) return false;
+    if (!shared_text || text_bits != 2) return false;
+    if (match < mismatch || match - mismatch > 255) return false;
+    if (aligner == NV_GOTOH ? (go > 0 || ge > 0) : (del > 0 || ins > 0)) return false;
+    if (type == NV_LOCAL && mismatch > 0) return false;
+    const int64_t mag = std::max<int64_t>({std::abs((int64_t)match), std::abs((int64_t)mismatch), std::abs((int64_t)go),
+                                           std::abs((int64_t)ge), std::abs((int64_t)del), std::abs((int64_t)ins), 1});
+    if (mag > 0x200) return false;   // a gap subtracted from NEG must not borrow across the halves
+    const int64_t vabs = ((int64_t)max_p + max_t + 2) * mag * 2;
+    const int64_t b = 0x400 + 2 * (std::abs((int64_t)go) + std::abs((int64_t)ge) + std::abs((int64_t)del) +
+                                   std::abs((int64_t)ins)) + vabs + 64;
+    if (b + vabs + 512 > 0x7BFF) return false;
+    *base = (uint32_t)b;
+    return true;
 }
 
 NvFn nv_lookup(bool gotoh, int type, bool mask, int G, int R) {
@@ -56,14 +97,20 @@ const NvShape *nv_shape(uint32_t max_p, uint32_t stride, bool per_pair_text, siz
 
 }  // namespace
 
-std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text) {
+std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text,
+                         uint32_t text_bits) {
     static const char *an[] = {"ed", "sw", "gotoh"}, *tn[] = {"global", "local", "semi"};
     if (al.aligner < 0 || al.aligner > 2 || al.type < 0 || al.type > 2) return "none";
     size_t lds = 0;
     const NvShape *sh = nv_shape(max_p, (std::max<uint32_t>(max_t, 1) + 7u) & ~7u, per_pair_text, &lds);
     if (!sh) return "none";
-    return std::string("nvbio_") + an[al.aligner] + "_" + tn[al.type] + (per_pair_text ? "" : "_shared") + "_G" +
-           std::to_string(sh->G) + "R" + std::to_string(sh->R);
+    const bool ed = al.aligner == NV_ED;
+    uint32_t base = 0;
+    const bool pk = nv16_ok(ed ? NV_SW : al.aligner, al.type, ed ? 0 : al.match, ed ? -1 : al.mismatch, al.gap_open,
+                            al.gap_ext, ed ? -1 : al.deletion, ed ? -1 : al.insertion, !per_pair_text, text_bits, max_p,
+                            max_t, &base);
+    return std::string(pk ? "nvbio16_" : "nvbio_") + an[al.aligner] + "_" + tn[al.type] + (per_pair_text ? "" : "_shared") +
+           "_G" + std::to_string(sh->G) + "R" + std::to_string(sh->R);
 }
 
 int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
@@ -96,6 +143,33 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
     const uint32_t stride = (std::max<uint32_t>(max_t, 1) + 7u) & ~7u;
     size_t lds = 0;
     const NvShape *sh = nv_shape(max_p, stride, txt.offsets != nullptr, &lds);
+    uint32_t base = 0;
+    if (sh && nv16_ok(gotoh ? NV_GOTOH : NV_SW, al.type, A.match, A.mismatch, A.go, A.ge, A.del, A.ins, !txt.offsets,
+                      txt.bits, max_p, max_t, &base)) {
+        Nv16Fn fn = nv16_lookup(gotoh ? NV_GOTOH : NV_SW, al.type, sh->G, sh->R);
+        if (fn) {
+            Nv16Args D;
+            D.pw = A.pw; D.poff = A.poff; D.pbits = A.pbits; D.pbig = A.pbig;
+            D.tw = A.tw; D.tbig = A.tbig; D.tlen0 = A.tlen0;
+            D.score = scores; D.score16 = scores16; D.n = n;
+            D.match = A.match; D.mismatch = A.mismatch; D.go = A.go; D.ge = A.ge; D.del = A.del; D.ins = A.ins;
+            D.base = base;
+            D.lds_cols = (A.tlen0 + (uint32_t)sh->G + 63u) & ~63u;
+            const size_t lds16 = (size_t)D.lds_cols * 4;
+            if (lds16 <= 160 * 1024) {
+                if (lds16 > 64 * 1024) {
+                    hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)lds16);
+                    if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+                }
+                const uint32_t per_block = 8 * (64 / sh->G);   // two pairs per lane group
+                hipLaunchKernelGGL(fn, dim3((n + per_block - 1) / per_block), dim3(256), lds16, st, D);
+                hipError_t e = hipGetLastError();
+                if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+                return GASALX_OK;
+            }
+        }
+    }
     NvFn fn = sh ? nv_lookup(gotoh, al.type, mask, sh->G, sh->R) : nullptr;
     if (fn) {
         A.lds_stride = stride;

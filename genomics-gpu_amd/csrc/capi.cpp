@@ -551,10 +551,10 @@ int gasalx_nv_score_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint
     return gx::nv_score_device(*al, n, *pat, *txt, scores, scores16, max_p, max_t, st);
 }
 
-int gasalx_nv_describe_plan(const gasalx_nv_aligner *al, uint32_t max_p, uint32_t max_t, int per_pair, char *buf,
-                            uint32_t buf_len) {
+int gasalx_nv_describe_plan(const gasalx_nv_aligner *al, uint32_t max_p, uint32_t max_t, int per_pair,
+                            uint32_t text_bits, char *buf, uint32_t buf_len) {
     if (!al || !buf || buf_len == 0) { gx::set_error("null argument"); return GASALX_EINVAL; }
-    std::snprintf(buf, buf_len, "%s", gx::nv_plan_name(*al, max_p, max_t, per_pair != 0).c_str());
+    std::snprintf(buf, buf_len, "%s", gx::nv_plan_name(*al, max_p, max_t, per_pair != 0, text_bits).c_str());
     return GASALX_OK;
 }
 

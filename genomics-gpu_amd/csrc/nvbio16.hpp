@@ -1,0 +1,180 @@
+// nvbio16.hpp — the nvbio front-end's scoring kernel (nvbio.hpp) with two pairs
+// per lane group: the pattern rows of pair 2p in the low 16-bit half of every
+// register, those of pair 2p + 1 in the high half, against the one text all
+// pairs share (sw-benchmark's layout: reads against one reference,
+// NvB/sw-benchmark/sw-benchmark.cu:355-443).  Same recurrences, boundaries and
+// sinks as nv_kernel; same lane-group wavefront (G lanes, R pattern rows per
+// lane, DPP hand-off of the bottom row).
+//
+// Arithmetic (as wavefront16.hpp): a stored value is value + B inside the
+// positive normal f16 range [0x0400, 0x7BFF], where v_pk_maximum3_f16 orders the
+// bit patterns like the integers: one instruction is an exact 3-way max on both
+// pairs, and 32-bit adds of a packed pair never carry or borrow across halves.
+// nvbio's -inf stand-in becomes NEG = 0x0400, below every reachable value; E and
+// F are floored there (LOCAL: at 0, exact for H because gaps never score > 0).
+//
+// Substitution: nvbio scores equality only (S = p == t ? match : mismatch).  The
+// text (2-bit, symbols 0..3) is staged in LDS as one 4-byte table per column,
+// byte l = (l == t) ? match - mismatch : 0, and a row's selector picks the byte
+// of its pattern symbol for each half (symbols >= 4, and pad rows, select the
+// constant 0: a mismatch, as nvbio's never-matching N); tmp = Hdg + byte +
+// mismatch is one v_add3.  Per cell of both pairs, Gotoh: v_perm, v_add3, F
+// (2 sub + maximum3), E (2 sub + maximum3), H (maximum3): 9 instructions.
+//
+// Sinks (sink_inl.h:59-68): LOCAL every cell (a running maximum3 over two cells
+// per instruction; pad rows and columns score <= 0 and never exceed a real cell,
+// which the host requires); SEMI_GLOBAL row M-1 of each pair at every column;
+// GLOBAL H(M-1, N-1).  The row M-1 of either half is picked through per-row
+// masks (mask[k] = 0xFFFF in the half whose last row is row k of this lane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nvbio.hpp"
+#include "wavefront16.hpp"
+
+namespace gx {
+
+struct Nv16Args {
+    const uint32_t *pw, *poff;      // pattern words, n + 1 symbol offsets
+    uint32_t pbits, pbig;
+    const uint32_t *tw;             // the shared text: 2-bit symbols
+    uint32_t tbig, tlen0;
+    int32_t *score;
+    int16_t *score16;
+    uint32_t n;
+    int32_t match, mismatch, go, ge, del, ins;
+    uint32_t base;                  // stored value of 0
+    uint32_t lds_cols;              // table entries staged (>= text length + G, multiple of 64)
+};
+
+__device__ __forceinline__ uint32_t nv16_dpp(uint32_t v) {   // lane i <- lane i-1 (DPP wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+template <int ALN, int TYPE, int G, int R>
+__global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t nvt[];
+    constexpr int P = 64 / G;
+    constexpr bool GOTOH = ALN == NV_GOTOH;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lg = lane & (G - 1), grp = lane / G;
+    const uint32_t pa = 2 * ((blockIdx.x * 4 + wave) * P + grp), pb = pa + 1;
+    const bool va = pa < A.n, vb = pb < A.n;
+    uint32_t Ma = 0, Mb = 0, poa = 0, pob = 0;
+    if (va) { poa = A.poff[pa]; Ma = A.poff[pa + 1] - poa; }
+    if (vb) { pob = A.poff[pb]; Mb = A.poff[pb + 1] - pob; }
+    const uint32_t N = A.tlen0;
+    // ---- the text as per-column tables (pads: all mismatch) ----
+    const uint32_t dm = (uint32_t)(A.match - A.mismatch);
+    for (uint32_t c = threadIdx.x; c < A.lds_cols; c += blockDim.x)
+        nvt[c] = c < N ? dm << (8 * nv_symbol(A.tw, 2, A.tbig, c)) : 0u;
+    __syncthreads();
+
+    const int32_t B = (int32_t)A.base;
+    const uint32_t BB = A.base * 0x10001u, NEG = 0x04000400u;
+    const uint32_t FLOOR = TYPE == NV_LOCAL ? BB : NEG;
+    const uint32_t MIS = (uint32_t)A.mismatch * 0x10001u;
+    const uint32_t GO = (uint32_t)(-A.go) * 0x10001u, GE = (uint32_t)(-A.ge) * 0x10001u;   // gaps <= 0
+    const uint32_t DEL = (uint32_t)(-A.del) * 0x10001u, INS = (uint32_t)(-A.ins) * 0x10001u;
+    auto pk = [&](int32_t v) { return (uint32_t)(v + B) * 0x10001u; };
+    // ---- the lane's pattern rows ----
+    const uint32_t r0 = lg * R;
+    const uint32_t last_a = Ma ? Ma - 1 : 0xFFFFFFFFu, last_b = Mb ? Mb - 1 : 0xFFFFFFFFu;
+    uint32_t sel[R], Hk[R], Ek[R], msk[R];
+    bool has_last = false;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t r = r0 + k;
+        const uint32_t ca = (va && r < Ma) ? nv_symbol(A.pw, A.pbits, A.pbig, poa + r) : 4u;
+        const uint32_t cb = (vb && r < Mb) ? nv_symbol(A.pw, A.pbits, A.pbig, pob + r) : 4u;
+        sel[k] = (ca < 4 ? ca : 0x0Cu) | 0x0C00u | ((cb < 4 ? cb : 0x0Cu) << 16) | 0x0C000000u;
+        if (GOTOH) {
+            Hk[k] = TYPE == NV_LOCAL ? BB : pk(A.go + A.ge * (int32_t)r);
+            Ek[k] = TYPE == NV_LOCAL ? BB : NEG;
+        } else {
+            Hk[k] = TYPE == NV_LOCAL ? BB : pk(A.ins * (int32_t)(r + 1));
+            Ek[k] = 0u;
+        }
+        msk[k] = (r == last_a ? 0x0000FFFFu : 0u) | (r == last_b ? 0xFFFF0000u : 0u);
+        has_last |= msk[k] != 0u;
+    }
+    const uint32_t nsteps = N + G - 1;
+    uint32_t best = TYPE == NV_LOCAL ? BB : NEG;   // stored; NEG = no cell seen (BestSink, sink_inl.h:38-40)
+    // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1); rH starts as the
+    // left boundary H(r0-1, -1), lane 1's diagonal at column 0 (nvbio.hpp)
+    const int32_t rb = (int32_t)r0 - 1;
+    uint32_t rH = (TYPE == NV_LOCAL || lg == 0) ? BB : pk(GOTOH ? A.go + A.ge * rb : A.ins * (rb + 1));
+    uint32_t rF = NEG, pH = BB;
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const int32_t c = (int32_t)s - (int32_t)lg;
+        uint32_t Hup, Fup, Hdg;
+        if (lg == 0) {
+            if (TYPE == NV_GLOBAL) {
+                Hup = pk(GOTOH ? A.go + A.ge * c : A.del * (c + 1));
+                Hdg = pk(GOTOH ? (c >= 1 ? A.go + A.ge * (c - 1) : 0) : A.del * c);
+            } else { Hup = BB; Hdg = BB; }
+            Fup = NEG;
+        } else { Hup = rH; Fup = rF; Hdg = pH; }
+        if (c >= 0 && (uint32_t)c < N) {
+            const uint32_t T = nvt[c];
+            uint32_t lbest = best;
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+                const uint32_t v = __builtin_amdgcn_perm(T, T, sel[k]);
+                const uint32_t tmp = Hdg + v + MIS;
+                uint32_t H;
+                if (GOTOH) {
+                    const uint32_t F = pk_max3(Fup - GE, Hup - GO, FLOOR);
+                    const uint32_t E = pk_max3(Ek[k] - GE, Hk[k] - GO, FLOOR);
+                    H = pk_max3(E, F, tmp);
+                    Ek[k] = E;
+                    Fup = F;
+                } else {
+                    H = pk_max3(Hup - INS, Hk[k] - DEL, tmp);
+                    if (TYPE == NV_LOCAL) H = pk_max3(H, BB, BB);
+                }
+                if (TYPE == NV_LOCAL) {   // two rows per maximum3: Hup is still row k - 1's H here
+                    if (k & 1) lbest = pk_max3(lbest, H, Hup);
+                    else if (k == R - 1) lbest = pk_max3(lbest, H, H);
+                }
+                Hdg = Hk[k];
+                Hk[k] = H;
+                Hup = H;
+            }
+            if (TYPE == NV_LOCAL) best = lbest;
+            if (TYPE != NV_LOCAL && has_last) {
+                uint32_t h = 0;
+#pragma unroll
+                for (int k = 0; k < R; ++k) h |= Hk[k] & msk[k];
+                if (TYPE == NV_SEMI) best = pk_max3(best, h, best);   // a half without its last row here: +0
+                else if ((uint32_t)c == N - 1) best = h;
+            }
+        }
+        pH = rH;
+        rH = nv16_dpp(Hk[R - 1]);
+        rF = nv16_dpp(Fup);
+    }
+    // LOCAL: the pair's best over its lanes
+    if (TYPE == NV_LOCAL) {
+#pragma unroll
+        for (int m = 1; m < G; m <<= 1) best = pk_max3(best, (uint32_t)__shfl_xor((int)best, m), best);
+    }
+    auto out = [&](bool valid, uint32_t pair, uint32_t M, uint32_t half, bool writer) {
+        if (!valid || !writer) return;
+        int32_t v = (int32_t)((best >> (16 * half)) & 0xFFFFu) - B;
+        if (M == 0) {
+            v = TYPE == NV_SEMI ? (N ? 0 : INT32_MIN)
+              : TYPE == NV_GLOBAL ? (N ? (GOTOH ? A.go + A.ge * (int32_t)(N - 1) : A.del * (int32_t)N) : INT32_MIN)
+                                  : INT32_MIN;
+        } else if (N == 0) v = INT32_MIN;
+        if (A.score) A.score[pair] = v;
+        if (A.score16) A.score16[pair] = (int16_t)v;
+    };
+    const bool wa = TYPE == NV_LOCAL ? lg == 0 : (Ma ? (Ma - 1) / R == lg : lg == 0);
+    const bool wb = TYPE == NV_LOCAL ? lg == 0 : (Mb ? (Mb - 1) / R == lg : lg == 0);
+    out(va, pa, Ma, 0, wa);
+    out(vb, pb, Mb, 1, wb);
+}
+
+}  // namespace gx

@@ -370,10 +370,11 @@ def describe_plan(params: Params, max_q: int, max_t: int) -> str:
     return buf.value.decode()
 
 
-def nv_describe_plan(aligner: "NvAligner", max_p: int, max_t: int, per_pair_texts: bool = False) -> str:
+def nv_describe_plan(aligner: "NvAligner", max_p: int, max_t: int, per_pair_texts: bool = False,
+                     text_bits: int = 2) -> str:
     buf = ctypes.create_string_buffer(128)
     al = aligner.cstruct()
-    _check(lib().gasalx_nv_describe_plan(ctypes.byref(al), max_p, max_t, int(per_pair_texts), buf, 128),
+    _check(lib().gasalx_nv_describe_plan(ctypes.byref(al), max_p, max_t, int(per_pair_texts), text_bits, buf, 128),
            "nv_describe_plan")
     return buf.value.decode()
 

@@ -247,10 +247,11 @@ int gasalx_nv_score_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner,
                            const gasalx_nv_strings *dev_patterns, const gasalx_nv_strings *dev_texts,
                            int32_t *dev_scores, int16_t *dev_scores16, uint32_t max_pattern_len,
                            uint32_t max_text_len, void *stream);
-/* The kernel shape a gasalx_nv_score_* call with these bounds runs (e.g.
- * "nvbio_gotoh_semi_shared_G8R19"); per_pair_texts = 0 for one shared text. */
+/* The kernel a gasalx_nv_score_* call with these bounds runs (e.g.
+ * "nvbio16_gotoh_semi_shared_G8R19": the packed kernel, two pairs per lane group;
+ * "nvbio_..." the int32 one); per_pair_texts = 0 for one shared text. */
 int gasalx_nv_describe_plan(const gasalx_nv_aligner *aligner, uint32_t max_pattern_len, uint32_t max_text_len,
-                            int per_pair_texts, char *buf, uint32_t buf_len);
+                            int per_pair_texts, uint32_t text_bits, char *buf, uint32_t buf_len);
 /* Host arrays in and out (words: the number of words of each set). */
 int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
                          const gasalx_nv_strings *patterns, uint64_t pattern_words, const gasalx_nv_strings *texts,

@@ -90,7 +90,7 @@ def test_pattern_lengths_every_shape(engine, m):
     T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
     for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
         _check(engine, _al(ALIGNERS[0], type_), G.PackedSet.pack(pats), T)
-    assert G.nv_describe_plan(ALIGNERS[0], m, 2200).startswith("nvbio_gotoh_global_shared_G")
+    assert G.nv_describe_plan(ALIGNERS[0], m, 2200).startswith("nvbio16_gotoh_global_shared_G")
 
 
 def test_empty_and_positive_scores(engine):
@@ -156,3 +156,46 @@ def test_sw_benchmark_driver(tmp_path):
              ("sw", "local"): G.NvAligner(G.NV_SW, G.NV_LOCAL, 2, -1, 0, 0, -1, -1)}
     for key, al in cases.items():
         assert np.array_equal(np.array(got[key], np.int16), O.nv_score(al, P, T).astype(np.int16)), key
+
+
+def _with_nv16(on):
+    if on:
+        os.environ.pop("GASALX_NV16", None)
+    else:
+        os.environ["GASALX_NV16"] = "0"
+
+
+def test_packed_plan_conditions():
+    # the packed kernel (nvbio16.hpp): one shared 2-bit text, gaps <= 0, LOCAL mismatch <= 0
+    g = ALIGNERS[0]
+    assert G.nv_describe_plan(g, 150, 1000).startswith("nvbio16_")
+    assert G.nv_describe_plan(g, 150, 1000, per_pair_texts=True).startswith("nvbio_")
+    assert G.nv_describe_plan(g, 150, 1000, text_bits=4).startswith("nvbio_")
+    assert G.nv_describe_plan(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 1, -1, 1, 1), 150, 1000).startswith("nvbio_")
+    assert G.nv_describe_plan(G.NvAligner(G.NV_SW, G.NV_LOCAL, 1, 2, 0, 0, -1, -1), 150, 1000).startswith("nvbio_")
+    assert G.nv_describe_plan(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), 150, 1000).startswith("nvbio16_ed_semi")
+
+
+@pytest.mark.parametrize("base", ALIGNERS, ids=["gotoh", "sw", "ed", "gotoh_b"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_packed_equals_int32_mixed_lengths(engine, base, type_):
+    # two pairs per lane group with different pattern lengths (each half has its own last
+    # row), odd pair counts, N and IUPAC pattern symbols (never match the 2-bit text)
+    rng = np.random.default_rng(500 + 7 * base.aligner + type_)
+    text = list(rng.integers(0, 4, 700))
+    pats = []
+    for i in range(1001):
+        p = _related(rng, text, int(rng.integers(1, 153)))
+        if i % 9 == 0:
+            p[int(rng.integers(0, len(p)))] = int(rng.integers(4, 16))
+        pats.append(np.array(p, np.uint32))
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
+    al = _al(base, type_)
+    g16 = _check(engine, al, P, T)
+    try:
+        _with_nv16(False)
+        g32 = engine.nv_score_host(al, P, T)
+    finally:
+        _with_nv16(True)
+    assert np.array_equal(g16, g32)
