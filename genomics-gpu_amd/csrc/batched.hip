@@ -32,31 +32,40 @@ NvFn nv_pick(int G, int R) {
 }
 
 using Nv16Fn = void (*)(Nv16Args);
-template <int ALN, int TYPE>
+template <int ALN, int TYPE, bool SHARED>
 Nv16Fn nv16_pick(int G, int R) {
-#define GX_CASE(g, r) if (G == g && R == r) return &nv16_kernel<ALN, TYPE, g, r>;
+#define GX_CASE(g, r) if (G == g && R == r) return &nv16_kernel<ALN, TYPE, g, r, SHARED>;
     GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 19) GX_CASE(8, 24) GX_CASE(16, 16) GX_CASE(16, 20)
     GX_CASE(32, 16) GX_CASE(64, 16)
 #undef GX_CASE
     return nullptr;
 }
-template <int ALN>
+template <int ALN, bool SHARED>
 Nv16Fn nv16_lookup_t(int type, int G, int R) {
-    return type == NV_GLOBAL ? nv16_pick<ALN, NV_GLOBAL>(G, R)
-         : type == NV_SEMI ? nv16_pick<ALN, NV_SEMI>(G, R) : nv16_pick<ALN, NV_LOCAL>(G, R);
+    return type == NV_GLOBAL ? nv16_pick<ALN, NV_GLOBAL, SHARED>(G, R)
+         : type == NV_SEMI ? nv16_pick<ALN, NV_SEMI, SHARED>(G, R) : nv16_pick<ALN, NV_LOCAL, SHARED>(G, R);
 }
-Nv16Fn nv16_lookup(int aln, int type, int G, int R) {
-    return aln == NV_GOTOH ? nv16_lookup_t<NV_GOTOH>(type, G, R) : nv16_lookup_t<NV_SW>(type, G, R);
+Nv16Fn nv16_lookup(int aln, int type, bool shared, int G, int R) {
+    if (shared)
+        return aln == NV_GOTOH ? nv16_lookup_t<NV_GOTOH, true>(type, G, R) : nv16_lookup_t<NV_SW, true>(type, G, R);
+    return aln == NV_GOTOH ? nv16_lookup_t<NV_GOTOH, false>(type, G, R) : nv16_lookup_t<NV_SW, false>(type, G, R);
+}
+// LDS of the packed kernel: one table per column of the shared text, or of every
+// pair's text (two pairs per lane group, 4 waves per block)
+uint32_t nv16_cols(bool shared, uint32_t max_t, int G) { return shared ? (max_t + G + 63u) & ~63u : (max_t + 3u) & ~3u; }
+size_t nv16_lds(bool shared, uint32_t max_t, int G) {
+    return (size_t)nv16_cols(shared, max_t, G) * 4 * (shared ? 1 : 4 * 2 * (64 / G));
 }
 
-// The packed kernel (nvbio16.hpp): one shared 2-bit text, gaps and (LOCAL) mismatches
-// <= 0, match - mismatch in a byte, and every value (bounded by (M + N + 2) * the
-// largest score magnitude) inside the 16-bit f16 window.  GASALX_NV16=0: int32 only.
+// The packed kernel (nvbio16.hpp): 2-bit texts, gaps and (LOCAL) mismatches <= 0,
+// match - mismatch in a byte, and every value (bounded by (M + N + 2) * the largest
+// score magnitude) inside the 16-bit f16 window.  GASALX_NV16=0: int32 only.
 bool nv16_ok(int aligner, int type, int32_t match, int32_t mismatch, int32_t go, int32_t ge, int32_t del, int32_t ins,
              bool shared_text, uint32_t text_bits, uint32_t max_p, uint32_t max_t, uint32_t *base) {
     const char *env = std::getenv("GASALX_NV16");
     if (env && std::atoi(env) == 0) return false;
-    if (!shared_text || text_bits != 2) return false;
+    (void)shared_text;
+    if (text_bits != 2) return false;
     if (match < mismatch || match - mismatch > 255) return false;
     if (aligner == NV_GOTOH ? (go > 0 || ge > 0) : (del > 0 || ins > 0)) return false;
     if (type == NV_LOCAL && mismatch > 0) return false;
@@ -109,7 +118,8 @@ std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t m
     const bool pk = nv16_ok(ed ? NV_SW : al.aligner, al.type, ed ? 0 : al.match, ed ? -1 : al.mismatch, al.gap_open,
                             al.gap_ext, ed ? -1 : al.deletion, ed ? -1 : al.insertion, !per_pair_text, text_bits, max_p,
                             max_t, &base);
-    return std::string(pk ? "nvbio16_" : "nvbio_") + an[al.aligner] + "_" + tn[al.type] + (per_pair_text ? "" : "_shared") +
+    const bool fits = nv16_lds(!per_pair_text, max_t, sh->G) <= 160 * 1024;
+    return std::string(pk && fits ? "nvbio16_" : "nvbio_") + an[al.aligner] + "_" + tn[al.type] + (per_pair_text ? "" : "_shared") +
            "_G" + std::to_string(sh->G) + "R" + std::to_string(sh->R);
 }
 
@@ -146,16 +156,17 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
     uint32_t base = 0;
     if (sh && nv16_ok(gotoh ? NV_GOTOH : NV_SW, al.type, A.match, A.mismatch, A.go, A.ge, A.del, A.ins, !txt.offsets,
                       txt.bits, max_p, max_t, &base)) {
-        Nv16Fn fn = nv16_lookup(gotoh ? NV_GOTOH : NV_SW, al.type, sh->G, sh->R);
+        const bool shared = !txt.offsets;
+        Nv16Fn fn = nv16_lookup(gotoh ? NV_GOTOH : NV_SW, al.type, shared, sh->G, sh->R);
         if (fn) {
             Nv16Args D;
             D.pw = A.pw; D.poff = A.poff; D.pbits = A.pbits; D.pbig = A.pbig;
-            D.tw = A.tw; D.tbig = A.tbig; D.tlen0 = A.tlen0;
+            D.tw = A.tw; D.toff = A.toff; D.tbig = A.tbig; D.tlen0 = A.tlen0;
             D.score = scores; D.score16 = scores16; D.n = n;
             D.match = A.match; D.mismatch = A.mismatch; D.go = A.go; D.ge = A.ge; D.del = A.del; D.ins = A.ins;
             D.base = base;
-            D.lds_cols = (A.tlen0 + (uint32_t)sh->G + 63u) & ~63u;
-            const size_t lds16 = (size_t)D.lds_cols * 4;
+            D.lds_cols = nv16_cols(shared, shared ? A.tlen0 : max_t, sh->G);
+            const size_t lds16 = nv16_lds(shared, shared ? A.tlen0 : max_t, sh->G);
             if (lds16 <= 160 * 1024) {
                 if (lds16 > 64 * 1024) {
                     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -38,21 +38,22 @@ namespace gx {
 struct Nv16Args {
     const uint32_t *pw, *poff;      // pattern words, n + 1 symbol offsets
     uint32_t pbits, pbig;
-    const uint32_t *tw;             // the shared text: 2-bit symbols
-    uint32_t tbig, tlen0;
+    const uint32_t *tw;             // 2-bit text symbols
+    const uint32_t *toff;           // n + 1 symbol offsets of per-pair texts (SHARED: unused)
+    uint32_t tbig, tlen0;           // tlen0: the shared text's length
     int32_t *score;
     int16_t *score16;
     uint32_t n;
     int32_t match, mismatch, go, ge, del, ins;
     uint32_t base;                  // stored value of 0
-    uint32_t lds_cols;              // table entries staged (>= text length + G, multiple of 64)
+    uint32_t lds_cols;              // table entries per staged text (>= its length, multiple of 4)
 };
 
 __device__ __forceinline__ uint32_t nv16_dpp(uint32_t v) {   // lane i <- lane i-1 (DPP wave_shr:1)
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-template <int ALN, int TYPE, int G, int R>
+template <int ALN, int TYPE, int G, int R, bool SHARED>
 __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t nvt[];
     constexpr int P = 64 / G;
@@ -64,12 +65,31 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     uint32_t Ma = 0, Mb = 0, poa = 0, pob = 0;
     if (va) { poa = A.poff[pa]; Ma = A.poff[pa + 1] - poa; }
     if (vb) { pob = A.poff[pb]; Mb = A.poff[pb + 1] - pob; }
-    const uint32_t N = A.tlen0;
-    // ---- the text as per-column tables (pads: all mismatch) ----
+    // ---- the text(s) as per-column tables (pads: all mismatch) ----
     const uint32_t dm = (uint32_t)(A.match - A.mismatch);
-    for (uint32_t c = threadIdx.x; c < A.lds_cols; c += blockDim.x)
-        nvt[c] = c < N ? dm << (8 * nv_symbol(A.tw, 2, A.tbig, c)) : 0u;
+    const uint32_t cols = A.lds_cols;
+    uint32_t Na = A.tlen0, Nb = A.tlen0, toa = 0, tob = 0;
+    const uint32_t *Ta = nvt, *Tb = nvt;
+    if (SHARED) {
+        for (uint32_t c = threadIdx.x; c < cols; c += blockDim.x)
+            nvt[c] = c < Na ? dm << (8 * nv_symbol(A.tw, 2, A.tbig, c)) : 0u;
+    } else {
+        // one slot per pair of the wave: slot 2*grp + half
+        Na = Nb = 0;
+        if (va) { toa = A.toff[pa]; Na = A.toff[pa + 1] - toa; }
+        if (vb) { tob = A.toff[pb]; Nb = A.toff[pb + 1] - tob; }
+        uint32_t *wl = nvt + (size_t)wave * 2 * P * cols;
+        for (uint32_t ps = 0; ps < 2u * P; ++ps) {   // uniform trip counts: shuffles see all lanes
+            const uint32_t src = (ps >> 1) * G;
+            const uint32_t pN = __shfl((ps & 1) ? Nb : Na, src), pto = __shfl((ps & 1) ? tob : toa, src);
+            for (uint32_t c = lane; c < cols; c += 64)
+                wl[ps * cols + c] = c < pN ? dm << (8 * nv_symbol(A.tw, 2, A.tbig, pto + c)) : 0u;
+        }
+        Ta = wl + 2 * grp * cols;
+        Tb = Ta + cols;
+    }
     __syncthreads();
+    const uint32_t N = max(Na, Nb);
 
     const int32_t B = (int32_t)A.base;
     const uint32_t BB = A.base * 0x10001u, NEG = 0x04000400u;
@@ -88,7 +108,9 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
         const uint32_t r = r0 + k;
         const uint32_t ca = (va && r < Ma) ? nv_symbol(A.pw, A.pbits, A.pbig, poa + r) : 4u;
         const uint32_t cb = (vb && r < Mb) ? nv_symbol(A.pw, A.pbits, A.pbig, pob + r) : 4u;
-        sel[k] = (ca < 4 ? ca : 0x0Cu) | 0x0C00u | ((cb < 4 ? cb : 0x0Cu) << 16) | 0x0C000000u;
+        // SHARED: both halves read the one table (v_perm(T, T, .)); otherwise the high
+        // half's bytes come from the second source, selectors 4..7
+        sel[k] = (ca < 4 ? ca : 0x0Cu) | 0x0C00u | ((cb < 4 ? cb + (SHARED ? 0u : 4u) : 0x0Cu) << 16) | 0x0C000000u;
         if (GOTOH) {
             Hk[k] = TYPE == NV_LOCAL ? BB : pk(A.go + A.ge * (int32_t)r);
             Ek[k] = TYPE == NV_LOCAL ? BB : NEG;
@@ -99,7 +121,14 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
         msk[k] = (r == last_a ? 0x0000FFFFu : 0u) | (r == last_b ? 0xFFFF0000u : 0u);
         has_last |= msk[k] != 0u;
     }
-    const uint32_t nsteps = N + G - 1;
+    uint32_t nmax = N;
+    if (!SHARED) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) nmax = max(nmax, (uint32_t)__shfl_xor(nmax, m));
+    }
+    const uint32_t nsteps = nmax + G - 1;
+    // per-half column limits of the sinks (SEMI: c < N of the half; GLOBAL: c == N - 1)
+    const uint32_t lastc_a = Na - 1, lastc_b = Nb - 1;
     uint32_t best = TYPE == NV_LOCAL ? BB : NEG;   // stored; NEG = no cell seen (BestSink, sink_inl.h:38-40)
     // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1); rH starts as the
     // left boundary H(r0-1, -1), lane 1's diagonal at column 0 (nvbio.hpp)
@@ -117,11 +146,11 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
             Fup = NEG;
         } else { Hup = rH; Fup = rF; Hdg = pH; }
         if (c >= 0 && (uint32_t)c < N) {
-            const uint32_t T = nvt[c];
+            const uint32_t T = Ta[c], T1 = SHARED ? T : Tb[c];
             uint32_t lbest = best;
 #pragma unroll
             for (int k = 0; k < R; ++k) {
-                const uint32_t v = __builtin_amdgcn_perm(T, T, sel[k]);
+                const uint32_t v = __builtin_amdgcn_perm(T1, T, sel[k]);
                 const uint32_t tmp = Hdg + v + MIS;
                 uint32_t H;
                 if (GOTOH) {
@@ -147,8 +176,15 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
                 uint32_t h = 0;
 #pragma unroll
                 for (int k = 0; k < R; ++k) h |= Hk[k] & msk[k];
-                if (TYPE == NV_SEMI) best = pk_max3(best, h, best);   // a half without its last row here: +0
-                else if ((uint32_t)c == N - 1) best = h;
+                if (TYPE == NV_SEMI) {   // a half without its last row here, or past its text: +0
+                    if (!SHARED) h &= ((uint32_t)c < Na ? 0x0000FFFFu : 0u) | ((uint32_t)c < Nb ? 0xFFFF0000u : 0u);
+                    best = pk_max3(best, h, best);
+                } else if (SHARED) {
+                    if ((uint32_t)c == N - 1) best = h;
+                } else {
+                    if ((uint32_t)c == lastc_a) best = (best & 0xFFFF0000u) | (h & 0x0000FFFFu);
+                    if ((uint32_t)c == lastc_b) best = (best & 0x0000FFFFu) | (h & 0xFFFF0000u);
+                }
             }
         }
         pH = rH;
@@ -160,7 +196,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
 #pragma unroll
         for (int m = 1; m < G; m <<= 1) best = pk_max3(best, (uint32_t)__shfl_xor((int)best, m), best);
     }
-    auto out = [&](bool valid, uint32_t pair, uint32_t M, uint32_t half, bool writer) {
+    auto out = [&](bool valid, uint32_t pair, uint32_t M, uint32_t N, uint32_t half, bool writer) {
         if (!valid || !writer) return;
         int32_t v = (int32_t)((best >> (16 * half)) & 0xFFFFu) - B;
         if (M == 0) {
@@ -173,8 +209,8 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     };
     const bool wa = TYPE == NV_LOCAL ? lg == 0 : (Ma ? (Ma - 1) / R == lg : lg == 0);
     const bool wb = TYPE == NV_LOCAL ? lg == 0 : (Mb ? (Mb - 1) / R == lg : lg == 0);
-    out(va, pa, Ma, 0, wa);
-    out(vb, pb, Mb, 1, wb);
+    out(va, pa, Ma, Na, 0, wa);
+    out(vb, pb, Mb, Nb, 1, wb);
 }
 
 }  // namespace gx

@@ -169,7 +169,8 @@ def test_packed_plan_conditions():
     # the packed kernel (nvbio16.hpp): one shared 2-bit text, gaps <= 0, LOCAL mismatch <= 0
     g = ALIGNERS[0]
     assert G.nv_describe_plan(g, 150, 1000).startswith("nvbio16_")
-    assert G.nv_describe_plan(g, 150, 1000, per_pair_texts=True).startswith("nvbio_")
+    assert G.nv_describe_plan(g, 150, 1000, per_pair_texts=True).startswith("nvbio_")   # tables beyond LDS
+    assert G.nv_describe_plan(g, 150, 400, per_pair_texts=True).startswith("nvbio16_gotoh_global_G8R19")
     assert G.nv_describe_plan(g, 150, 1000, text_bits=4).startswith("nvbio_")
     assert G.nv_describe_plan(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 1, -1, 1, 1), 150, 1000).startswith("nvbio_")
     assert G.nv_describe_plan(G.NvAligner(G.NV_SW, G.NV_LOCAL, 1, 2, 0, 0, -1, -1), 150, 1000).startswith("nvbio_")
@@ -192,6 +193,31 @@ def test_packed_equals_int32_mixed_lengths(engine, base, type_):
     P = G.PackedSet.pack(pats, bits=4, big_endian=True)
     T = G.PackedSet.pack([np.array(text, np.uint32)], bits=2, big_endian=False, shared=True)
     al = _al(base, type_)
+    g16 = _check(engine, al, P, T)
+    try:
+        _with_nv16(False)
+        g32 = engine.nv_score_host(al, P, T)
+    finally:
+        _with_nv16(True)
+    assert np.array_equal(g16, g32)
+
+
+@pytest.mark.parametrize("base", ALIGNERS, ids=["gotoh", "sw", "ed", "gotoh_b"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_packed_per_pair_texts_equals_int32(engine, base, type_):
+    # per-pair texts of different lengths in the two halves of a lane group (each half's
+    # own sink column), empty texts and patterns, odd counts
+    rng = np.random.default_rng(900 + 7 * base.aligner + type_)
+    pats, texts = [], []
+    for i in range(777):
+        t = list(rng.integers(0, 4, int(rng.integers(0 if i % 50 == 0 else 1, 380))))
+        texts.append(np.array(t, np.uint32))
+        m = 0 if i % 61 == 0 else int(rng.integers(1, 140))
+        pats.append(np.array(_related(rng, t, m) if t else list(rng.integers(0, 4, m)), np.uint32))
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+    al = _al(base, type_)
+    assert G.nv_describe_plan(al, 140, 380, per_pair_texts=True).startswith("nvbio16_")
     g16 = _check(engine, al, P, T)
     try:
         _with_nv16(False)
