@@ -180,6 +180,7 @@ static bool band16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
     if (p.match < 0 || p.mismatch < 0 || p.gap_open < 0 || p.gap_extend < 0) return false;
     if (p.match + p.mismatch > 255 || p.gap_open + p.gap_extend > 4096) return false;
     if (p.has_n_penalty && p.n_penalty < 0) return false;
+    if (q8 > 65535) return false;   // the first-maximum row is tracked in 16 bits
     const int64_t hmax = (int64_t)p.match * std::min(q8, t8);
     return hmax + band16_base(p) <= 0x7BFF && hmax * 8 + 7 + 0x400 <= 0x7BFF;
 }
