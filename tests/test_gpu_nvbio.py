@@ -225,3 +225,17 @@ def test_packed_per_pair_texts_equals_int32(engine, base, type_):
     finally:
         _with_nv16(True)
     assert np.array_equal(g16, g32)
+
+
+def test_packed_value_window_edge(engine):
+    # patterns of 1,024 against one 6,000-symbol text: (M + N + 2) * 2 * mag = 14,052,
+    # near the packed kernel's window; GLOBAL reaches about -(N + M)
+    rng = np.random.default_rng(4242)
+    text = list(rng.integers(0, 4, 6000))
+    pats = [np.array(_related(rng, text, 1024 - int(rng.integers(0, 40))), np.uint32) for _ in range(40)]
+    P = G.PackedSet.pack(pats)
+    T = G.PackedSet.pack([np.array(text, np.uint32)], 2, False, shared=True)
+    for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+        al = G.NvAligner(G.NV_SW, type_, 1, -1, 0, 0, -1, -1)
+        assert G.nv_describe_plan(al, 1024, 6000).startswith("nvbio16_")
+        _check(engine, al, P, T)

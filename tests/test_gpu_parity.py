@@ -404,6 +404,21 @@ def test_banded16_n_bases_and_iupac(engine):
         check(engine, b, algo=G.BANDED, k_band=16, **kw)
 
 
+def test_banded16_value_window_edge(engine):
+    # H up to match * 1,704 = 3,408 (the key limit is 3,455): long identical-ish pairs with
+    # match 2, at the top of the packed value window
+    rng = np.random.default_rng(99)
+    qs, ts = [], []
+    for _ in range(64):
+        q = helpers.random_seq(rng, 1700)
+        qs.append(q)
+        ts.append(helpers.mutate(rng, q, sub=0.005, indel=0.0)[:1704])
+    b = G.Batch.from_pairs(qs, ts)
+    kw = dict(algo=G.BANDED, k_band=64, match=2, mismatch=3, gap_open=5, gap_extend=2)
+    assert G.describe_plan(G.make_params(**kw), 1700, 1704).startswith("banded16")
+    check(engine, b, **kw)
+
+
 def test_banded16_equals_int32_kernel(engine):
     # the packed kernel and the reference-shaped int32 kernel on the same batch
     b = G.Batch.synth(4, 20000, 0x5EED0004)
