@@ -356,7 +356,7 @@ def test_banded16_plan():
         "generic_banded"
 
 
-@pytest.mark.parametrize("k_band", [8, 16, 24, 64, 400])
+@pytest.mark.parametrize("k_band", [0, 4, 8, 16, 24, 64, 400])
 @pytest.mark.parametrize("scores", [{}, dict(match=2, mismatch=3, gap_open=5, gap_extend=2),
                                     dict(match=3, mismatch=1, gap_open=1, gap_extend=1, n_penalty=2)])
 def test_banded16_config4_geometry(engine, k_band, scores):
