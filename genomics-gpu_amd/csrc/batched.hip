@@ -68,7 +68,7 @@ bool nv16_ok(int aligner, int type, int32_t match, int32_t mismatch, int32_t go,
     if (text_bits != 2) return false;
     if (match < mismatch || match - mismatch > 255) return false;
     if (aligner == NV_GOTOH ? (go > 0 || ge > 0) : (del > 0 || ins > 0)) return false;
-    if (type == NV_LOCAL && mismatch > 0) return false;
+    if (mismatch > 0 || mismatch < -255) return false;   // virtual rows score the byte |mismatch|
     const int64_t mag = std::max<int64_t>({std::abs((int64_t)match), std::abs((int64_t)mismatch), std::abs((int64_t)go),
                                            std::abs((int64_t)ge), std::abs((int64_t)del), std::abs((int64_t)ins), 1});
     if (mag > 0x200) return false;   // a gap subtracted from NEG must not borrow across the halves

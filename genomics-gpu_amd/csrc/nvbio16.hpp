@@ -99,26 +99,37 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     const uint32_t DEL = (uint32_t)(-A.del) * 0x10001u, INS = (uint32_t)(-A.ins) * 0x10001u;
     auto pk = [&](int32_t v) { return (uint32_t)(v + B) * 0x10001u; };
     // ---- the lane's pattern rows ----
-    const uint32_t r0 = lg * R;
+    // BOT (one shared text, SEMI_GLOBAL): rows bottom-aligned per half, so both pairs'
+    // last row M-1 is row R-1 of lane G-1 and the sink is one maximum per step.  The
+    // rows above row 0 are virtual: they score every column with the constant byte
+    // |mismatch| (v_perm's second source, selector 4), so tmp = Hdg and, from the free
+    // top boundary H = 0 (F = -inf), each passes H = 0 down unchanged (E and F stay
+    // below it: gap scores <= 0) — row 0 sees exactly nvbio's boundary.
+    constexpr bool BOT = SHARED && TYPE == NV_SEMI;
+    const uint32_t VCONST = (uint32_t)(-A.mismatch);
+    const int32_t ra0 = (int32_t)(lg * R) - (BOT ? (int32_t)(G * R - Ma) : 0);
+    const int32_t rb0 = (int32_t)(lg * R) - (BOT ? (int32_t)(G * R - Mb) : 0);
     const uint32_t last_a = Ma ? Ma - 1 : 0xFFFFFFFFu, last_b = Mb ? Mb - 1 : 0xFFFFFFFFu;
     uint32_t sel[R], Hk[R], Ek[R], msk[R];
     bool has_last = false;
+    auto left = [&](int32_t r) {   // H(r, -1); virtual rows: 0
+        if (TYPE == NV_LOCAL || r < 0) return 0;
+        return GOTOH ? A.go + A.ge * r : A.ins * (r + 1);
+    };
+    auto pk2 = [&](int32_t a, int32_t b) { return (uint32_t)(a + B) | ((uint32_t)(b + B) << 16); };
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const uint32_t r = r0 + k;
-        const uint32_t ca = (va && r < Ma) ? nv_symbol(A.pw, A.pbits, A.pbig, poa + r) : 4u;
-        const uint32_t cb = (vb && r < Mb) ? nv_symbol(A.pw, A.pbits, A.pbig, pob + r) : 4u;
-        // SHARED: both halves read the one table (v_perm(T, T, .)); otherwise the high
-        // half's bytes come from the second source, selectors 4..7
-        sel[k] = (ca < 4 ? ca : 0x0Cu) | 0x0C00u | ((cb < 4 ? cb + (SHARED ? 0u : 4u) : 0x0Cu) << 16) | 0x0C000000u;
-        if (GOTOH) {
-            Hk[k] = TYPE == NV_LOCAL ? BB : pk(A.go + A.ge * (int32_t)r);
-            Ek[k] = TYPE == NV_LOCAL ? BB : NEG;
-        } else {
-            Hk[k] = TYPE == NV_LOCAL ? BB : pk(A.ins * (int32_t)(r + 1));
-            Ek[k] = 0u;
-        }
-        msk[k] = (r == last_a ? 0x0000FFFFu : 0u) | (r == last_b ? 0xFFFF0000u : 0u);
+        const int32_t ra = ra0 + k, rb = rb0 + k;
+        const uint32_t ca = (va && ra >= 0 && ra < (int32_t)Ma) ? nv_symbol(A.pw, A.pbits, A.pbig, poa + ra) : 4u;
+        const uint32_t cb = (vb && rb >= 0 && rb < (int32_t)Mb) ? nv_symbol(A.pw, A.pbits, A.pbig, pob + rb) : 4u;
+        // SHARED: both halves read the one table (v_perm(VCONST, T, .)); otherwise the
+        // high half's bytes come from the second source, selectors 4..7
+        const uint32_t sa = ra < 0 ? 4u : (ca < 4 ? ca : 0x0Cu);
+        const uint32_t sb = rb < 0 ? 4u : (cb < 4 ? cb + (SHARED ? 0u : 4u) : 0x0Cu);
+        sel[k] = sa | 0x0C00u | (sb << 16) | 0x0C000000u;
+        Hk[k] = pk2(left(ra), left(rb));
+        Ek[k] = GOTOH ? (TYPE == NV_LOCAL ? BB : NEG) : 0u;
+        msk[k] = ((uint32_t)ra == last_a ? 0x0000FFFFu : 0u) | ((uint32_t)rb == last_b ? 0xFFFF0000u : 0u);
         has_last |= msk[k] != 0u;
     }
     uint32_t nmax = N;
@@ -132,8 +143,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     uint32_t best = TYPE == NV_LOCAL ? BB : NEG;   // stored; NEG = no cell seen (BestSink, sink_inl.h:38-40)
     // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1); rH starts as the
     // left boundary H(r0-1, -1), lane 1's diagonal at column 0 (nvbio.hpp)
-    const int32_t rb = (int32_t)r0 - 1;
-    uint32_t rH = (TYPE == NV_LOCAL || lg == 0) ? BB : pk(GOTOH ? A.go + A.ge * rb : A.ins * (rb + 1));
+    uint32_t rH = lg == 0 ? BB : pk2(left(ra0 - 1), left(rb0 - 1));
     uint32_t rF = NEG, pH = BB;
     for (uint32_t s = 0; s < nsteps; ++s) {
         const int32_t c = (int32_t)s - (int32_t)lg;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
             Fup = NEG;
         } else { Hup = rH; Fup = rF; Hdg = pH; }
         if (c >= 0 && (uint32_t)c < N) {
-            const uint32_t T = Ta[c], T1 = SHARED ? T : Tb[c];
+            const uint32_t T = Ta[c], T1 = SHARED ? VCONST : Tb[c];
             uint32_t lbest = best;
 #pragma unroll
             for (int k = 0; k < R; ++k) {
@@ -172,7 +182,9 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
                 Hup = H;
             }
             if (TYPE == NV_LOCAL) best = lbest;
-            if (TYPE != NV_LOCAL && has_last) {
+            if (BOT) {
+                if (lg == G - 1) best = pk_max3(best, Hk[R - 1], best);
+            } else if (TYPE != NV_LOCAL && has_last) {
                 uint32_t h = 0;
 #pragma unroll
                 for (int k = 0; k < R; ++k) h |= Hk[k] & msk[k];
@@ -207,8 +219,8 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
         if (A.score) A.score[pair] = v;
         if (A.score16) A.score16[pair] = (int16_t)v;
     };
-    const bool wa = TYPE == NV_LOCAL ? lg == 0 : (Ma ? (Ma - 1) / R == lg : lg == 0);
-    const bool wb = TYPE == NV_LOCAL ? lg == 0 : (Mb ? (Mb - 1) / R == lg : lg == 0);
+    const bool wa = TYPE == NV_LOCAL ? lg == 0 : BOT ? lg == G - 1 : (Ma ? (Ma - 1) / R == lg : lg == 0);
+    const bool wb = TYPE == NV_LOCAL ? lg == 0 : BOT ? lg == G - 1 : (Mb ? (Mb - 1) / R == lg : lg == 0);
     out(va, pa, Ma, Na, 0, wa);
     out(vb, pb, Mb, Nb, 1, wb);
 }
