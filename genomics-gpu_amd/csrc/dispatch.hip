@@ -544,7 +544,18 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         if (p.algo == 6) {
             const size_t ke = (size_t)(shape.max_q + 8) * n;
             HIPCHK(ws.rows_h.reserve(ke * 8));
-            gen_ksw_kernel<<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.as<int2>());
+            // 8-bit (h, e) entries, then 16-bit, then int2, each for the pairs whose score
+            // bound does not fit the level before (GASALX_KSW_NARROW=0: int2 only, A/B)
+            const char *kn = std::getenv("GASALX_KSW_NARROW");
+            uint8_t *todo = nullptr;
+            if (!(kn && std::atoi(kn) == 0)) {
+                HIPCHK(ws.misc.reserve(n));
+                HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
+                todo = ws.misc.as<uint8_t>();
+                gen_ksw_kernel<0><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
+                gen_ksw_kernel<1><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
+            }
+            gen_ksw_kernel<2><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
         } else {
             HIPCHK(ws.rows_h.reserve(rows_elems * 2));
             HIPCHK(ws.rows_e.reserve(rows_elems * 2));

@@ -420,23 +420,52 @@ __device__ __forceinline__ int ksw_wave_max(int v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int2 *ehp) {
+// The entry width is a level: 0 = (h, e) as two uint8 in 16 bits, 1 = two uint16 in
+// 32 bits, 2 = int2 (both values are >= 0 and at most h0 + match * min(qlen, tlen)).
+// The loop is bound by its entry traffic, so narrower entries run faster; a pair whose
+// bound does not fit its level is flagged (todo = level + 1) for the next instance.
+template <int LEVEL>
+__global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint8_t *todo) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = tid < A.n;   // lanes past n run the wave's row loop without work
+    // lanes past n, and pairs of the other instance, run the wave's row loop without work
+    bool live = tid < A.n && (todo ? todo[tid] == LEVEL : LEVEL == 2);
+    if (LEVEL < 2 && live) {
+        const uint64_t bound = (uint64_t)(A.seed ? A.seed[tid] : 0u) +
+                               (uint64_t)max(A.a, 0) * min(A.qlen[tid], A.tlen[tid]);
+        if (bound > (LEVEL == 0 ? 255u : 65535u)) { todo[tid] = LEVEL + 1; live = false; }
+    }
     const uint32_t qlen = live ? A.qlen[tid] : 0u, tlen = live ? A.tlen[tid] : 0u;
     const uint32_t *qw = A.qw + (live ? A.qoff[tid] >> 3 : 0u);
     const uint32_t *tw = A.tw + (live ? A.toff[tid] >> 3 : 0u);
     const uint32_t h0 = (live && A.seed) ? A.seed[tid] : 0u;
     const int o_del = A.o, o_ins = A.o, e_del = A.e, e_ins = A.e;
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
-#define EHP(j) ehp[(size_t)(j) * A.n + tid]
+    int2 *ehw = reinterpret_cast<int2 *>(ehv);
+    uint32_t *ehn = reinterpret_cast<uint32_t *>(ehv);
+    uint16_t *ehb = reinterpret_cast<uint16_t *>(ehv);
+    auto put = [&](int j, int h, int e) {
+        if (LEVEL == 0) ehb[(size_t)j * A.n + tid] = (uint16_t)((uint32_t)h | ((uint32_t)e << 8));
+        else if (LEVEL == 1) ehn[(size_t)j * A.n + tid] = (uint32_t)h | ((uint32_t)e << 16);
+        else ehw[(size_t)j * A.n + tid] = make_int2(h, e);
+    };
+    auto get = [&](int j) {
+        if (LEVEL == 0) {
+            const uint32_t v = ehb[(size_t)j * A.n + tid];
+            return make_int2((int)(v & 0xFFu), (int)(v >> 8));
+        }
+        if (LEVEL == 1) {
+            const uint32_t v = ehn[(size_t)j * A.n + tid];
+            return make_int2((int)(v & 0xFFFFu), (int)(v >> 16));
+        }
+        return ehw[(size_t)j * A.n + tid];
+    };
     if (live) {
-        for (uint32_t j = 0; j < qlen + 2; j++) EHP(j) = make_int2(0, 0);
+        for (uint32_t j = 0; j < qlen + 2; j++) put((int)j, 0, 0);
         int h = (int32_t)h0;       // the first row (:72-76)
-        EHP(0) = make_int2(h, 0);
+        put(0, h, 0);
         h = (h0 > (uint32_t)oe_ins) ? (int32_t)(h0 - (uint32_t)oe_ins) : 0;
-        EHP(1) = make_int2(h, 0);
-        for (int j = 2; j <= (int)qlen && h > e_ins; ++j) { h -= e_ins; EHP(j) = make_int2(h, 0); }
+        put(1, h, 0);
+        for (int j = 2; j <= (int)qlen && h > e_ins; ++j) { h -= e_ins; put(j, h, 0); }
     }
     int max_ = (int32_t)h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1;
     int beg = 0, end = (int)qlen;
@@ -465,7 +494,7 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int2 *ehp) {
             if ((j & 7) == 0) rpac = qw[(uint32_t)j >> 3];
             if (j < beg) continue;
             const uint32_t rbase = (rpac >> (28 - 4 * (j & 7))) & 0x0F;
-            const int2 v = EHP(j);
+            const int2 v = get(j);
             int h, M = v.x, e = v.y;
             const int hs = h1;           // H(i, j-1), stored for the next row
             M = M ? M + g_sub_local(A, rbase, gbase) : 0;
@@ -476,12 +505,12 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int2 *ehp) {
             m = m > h ? m : h;
             t = M - oe_del; t = t > 0 ? t : 0;
             e -= e_del; e = e > t ? e : t;
-            EHP(j) = make_int2(hs, e);
+            put(j, hs, e);
             if ((hs | e) != 0) { first = min(first, j); last = j; }   // h, e >= 0
             t = M - oe_ins; t = t > 0 ? t : 0;
             f -= e_ins; f = f > t ? f : t;
         }
-        EHP(end) = make_int2(h1, 0);
+        put(end, h1, 0);
         if (h1 != 0) { first = min(first, end); last = end; }
         // the reference's column index after its loops is qlen exactly when the
         // row ended at qlen or qlen is a multiple of 8 (Q16's extra word)
@@ -505,7 +534,6 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, int2 *ehp) {
         if (A.qend) A.qend[tid] = (int32_t)qlen;
         if (A.tend) A.tend[tid] = max_ie + 1;
     }
-#undef EHP
 }
 
 // ------------------------------------------------------------- traceback ----

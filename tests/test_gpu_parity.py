@@ -440,7 +440,9 @@ def test_ksw(engine):
 
 
 @pytest.mark.parametrize("lens,seeds", [((1, 40), (0, 5)), ((8, 8), (0, 30)), ((64, 64), (0, 100)),
-                                        ((100, 260), (0, 200)), ((150, 150), (10, 11))])
+                                        ((100, 260), (0, 200)), ((150, 150), (10, 11)),
+                                        ((100, 200), (65000, 66000)),    # 16-bit entries overflow: int2 kernel
+                                        ((60, 160), (0, 300))])          # mixed 8- and 16-bit levels in one batch
 def test_ksw_trimming(engine, lens, seeds):
     # beg/end trimming (ksw_kernel_template.h:181-186) tracked in registers: rows that die
     # early (small seeds), query lengths that are multiples of 8 (the gscore test after the
