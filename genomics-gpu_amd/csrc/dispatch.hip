@@ -8,6 +8,7 @@
 #include <string>
 
 #include "banded16.hpp"
+#include "local16.hpp"
 #include "engine.hpp"
 #include "generic.hpp"
 #include "pairhmm.hpp"
@@ -185,6 +186,24 @@ static bool band16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
     return hmax + band16_base(p) <= 0x7BFF && hmax * 8 + 7 + 0x400 <= 0x7BFF;
 }
 
+// Packed LOCAL second-best kernel (local16.hpp): table bytes s + K in [0, 255]
+// (K = max(0, b, N_PENALTY)), stored values B + [0, Hmax] and keys H*8 + 7 +
+// 0x400 inside [0x0400, 0x7BFF].  GASALX_LOCAL16=0 keeps every pair on the int32
+// kernel (A/B runs).
+static int32_t local16_sn(const gasalx_params &p) { return p.has_n_penalty ? -p.n_penalty : 0; }
+static uint32_t local16_k(const gasalx_params &p) { return (uint32_t)std::max({0, p.mismatch, -local16_sn(p)}); }
+static uint32_t local16_base(const gasalx_params &p) { return 0x400u + (uint32_t)(p.gap_open + p.gap_extend) + local16_k(p); }
+static bool local16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
+    const char *env = std::getenv("GASALX_LOCAL16");
+    if (env && std::atoi(env) == 0) return false;
+    if (p.match < 0 || p.gap_open < 0 || p.gap_extend < 0 || p.gap_open + p.gap_extend > 4096) return false;
+    const int64_t k = local16_k(p), sn = local16_sn(p);
+    if (p.match + k > 255 || k - p.mismatch > 255 || sn + k > 255) return false;
+    if (q8 > 65535 || t8 / 8 > 65535) return false;   // rows and strips are tracked in 16 bits
+    const int64_t hmax = (int64_t)std::max<int64_t>(p.match, sn) * std::min(q8, t8);
+    return hmax + local16_base(p) <= 0x7BFF && hmax * 8 + 7 + 0x400 <= 0x7BFF;
+}
+
 Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     Plan pl;
     const uint32_t q8 = pad8(s.max_q), t8 = pad8(s.max_t);
@@ -267,6 +286,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         if (p.algo == 5 && band16_ok(p, q8, t8)) {
             pl.band16 = true;
             pl.name = "banded16_local";
+        }
+        if (p.algo == 3 && p.second_best && p.start_pos == 0 && local16_ok(p, q8, t8)) {
+            pl.local16 = true;
+            pl.name = "local16_second";
         }
     } else {
         pl.kind = PLAN_NONE;
@@ -400,6 +423,27 @@ static bool sort_wanted(const BatchShape &s) {
         return e ? std::atoi(e) : -1;
     }();
     return force < 0 ? s.sort : force != 0;
+}
+
+// Uneven lengths, two pairs per lane (banded16 / local16): pair up slots of equal
+// tile geometry (QR, TR) by a counting sort on it.  *perm stays NULL (identity)
+// for even batches, small ones and geometry counts whose histogram exceeds LDS.
+static int geometry_perm(Workspace &ws, const gasalx_batch &b, const BatchShape &shape, uint32_t n, hipStream_t st,
+                         const uint32_t **perm_out) {
+    *perm_out = nullptr;
+    const uint32_t trw = pad8(shape.max_t) / 8, nkeys = (pad8(shape.max_q) / 8) * trw;
+    const size_t sh = (size_t)(nkeys + 1) * 4;
+    if (!(sort_wanted(shape) && n >= 4096 && 2 * sh <= 64 * 1024)) return GASALX_OK;
+    HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + 2 * sh + 64));
+    uint32_t *perm = ws.sort_meta.as<uint32_t>(), *klen = perm + n, *hist = klen + n, *cursor = hist + nkeys + 1;
+    band16_key_kernel<<<grid_for(n, 256), 256, 0, st>>>(b.q_lens, b.t_lens, n, trw, klen);
+    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, hist);
+    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nkeys + 1);
+    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, cursor, perm);
+    HIPCHK(hipGetLastError());
+    *perm_out = perm;
+    return GASALX_OK;
 }
 
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
@@ -560,7 +604,32 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             HIPCHK(ws.rows_h.reserve(rows_elems * 2));
             HIPCHK(ws.rows_e.reserve(rows_elems * 2));
             A.rowH = ws.rows_h.as<int16_t>(); A.rowE = ws.rows_e.as<int16_t>();
-            if (p.algo == 3) gen_local_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            if (p.algo == 3) {
+                if (pl.local16) {
+                    Local16Args D;
+                    std::memset(&D, 0, sizeof(D));
+                    D.qw = A.qw; D.tw = A.tw;
+                    D.qoff = b.q_offsets; D.toff = b.t_offsets; D.qlen = b.q_lens; D.tlen = b.t_lens;
+                    D.score = out.aln_score; D.qend = qend; D.tend = tend;
+                    D.score2 = out.aln_score2; D.qend2 = out.q_end2; D.tend2 = out.t_end2;
+                    D.n = n; D.n_lanes = (n + 1) / 2;
+                    D.a = p.match; D.b = p.mismatch; D.oe = p.gap_open + p.gap_extend; D.e = p.gap_extend;
+                    D.nval = A.nval; D.sn = local16_sn(p); D.k = local16_k(p); D.base = local16_base(p);
+                    HIPCHK(ws.misc.reserve(n));
+                    HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
+                    D.todo = ws.misc.as<uint8_t>();
+                    HIPCHK(ws.aux.reserve((size_t)q8 * D.n_lanes * 8 + 64));
+                    D.rows = ws.aux.as<uint2>();
+                    {
+                        const int rc = geometry_perm(ws, b, shape, n, st, &D.perm);
+                        if (rc) return rc;
+                    }
+                    local2nd16_kernel<<<grid_for(D.n_lanes, 256), 256, 0, st>>>(D);
+                    HIPCHK(hipGetLastError());
+                    A.todo = D.todo;
+                }
+                gen_local_kernel<<<grid_for(n, 256), 256, 0, st>>>(A);
+            }
             else if (p.algo == 2) {
                 if (p.start_pos == 1) {
                     HIPCHK(ws.rev.reserve((size_t)2 * A.rev_words * n * 4));
@@ -582,20 +651,9 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                     D.todo = ws.misc.as<uint8_t>();
                     HIPCHK(ws.aux.reserve((size_t)q8 * D.n_lanes * 8 + 64));
                     D.rows = ws.aux.as<uint2>();
-                    // uneven lengths: pair up slots of equal tile geometry (counting sort)
-                    const uint32_t trw = t8 / 8, nkeys = (q8 / 8) * trw;
-                    const size_t sh = (size_t)(nkeys + 1) * 4;
-                    if (sort_wanted(shape) && n >= 4096 && 2 * sh <= 64 * 1024) {
-                        HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + 2 * sh + 64));
-                        uint32_t *perm = ws.sort_meta.as<uint32_t>(), *klen = perm + n, *hist = klen + n,
-                                 *cursor = hist + nkeys + 1;
-                        band16_key_kernel<<<grid_for(n, 256), 256, 0, st>>>(b.q_lens, b.t_lens, n, trw, klen);
-                        HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-                        rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, hist);
-                        rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nkeys + 1);
-                        rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys,
-                                                                                  cursor, perm);
-                        D.perm = perm;
+                    {
+                        const int rc = geometry_perm(ws, b, shape, n, st, &D.perm);
+                        if (rc) return rc;
                     }
                     band16_kernel<<<grid_for(D.n_lanes, 256), 256, 0, st>>>(D);
                     HIPCHK(hipGetLastError());

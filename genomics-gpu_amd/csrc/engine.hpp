@@ -53,6 +53,7 @@ struct Plan {
     size_t lds_bytes = 0;
     bool need_pack = false; // generic kernels / reverse-complement need packed words
     bool band16 = false;    // banded: two pairs per lane in 16-bit halves (banded16.hpp), int32 fallback
+    bool local16 = false;   // LOCAL second best: two pairs per lane in 16-bit halves (local16.hpp), int32 fallback
     std::string name;
 };
 

@@ -31,7 +31,7 @@ struct GenArgs {
     uint32_t n;
     int32_t a, b, o, e, nval, has_npen, npen;
     int32_t start_pos, second, head, tail, kbw, maxq;
-    const uint8_t *todo;              // banded: only the pairs the packed kernel declined (NULL: all)
+    const uint8_t *todo;              // banded / local: only the pairs the packed kernel declined (NULL: all)
 };
 
 __device__ __forceinline__ uint32_t gcode(const uint32_t *w, uint32_t pos) {
@@ -47,6 +47,7 @@ __device__ __forceinline__ int32_t g_sub_local(const GenArgs &A, uint32_t q, uin
 __global__ __launch_bounds__(256) void gen_local_kernel(GenArgs A) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= A.n) return;
+    if (A.todo && !A.todo[tid]) return;   // aligned by local2nd16_kernel
     const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
     const uint32_t *qw = A.qw + (A.qoff[tid] >> 3);
     const uint32_t *tw = A.tw + (A.toff[tid] >> 3);

@@ -73,7 +73,9 @@ def test_plan_selection_cpu_only():
         "wavefront16_semi_start_G8R23"
     assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL, start_pos=G.WITH_START, tail=G.QUERY), 150, 182) == \
         "generic_semi"
-    assert G.describe_plan(G.make_params(algo=G.LOCAL, second_best=1), 150, 150) == "generic_local"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, second_best=1), 150, 150) == "local16_second"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, second_best=1, start_pos=G.WITH_START), 150, 150) == \
+        "generic_local"
     assert G.describe_plan(G.make_params(algo=G.KSW), 150, 150) == "generic_ksw"
     assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300) == \
         "wavefront16_global_tb_G16R20"

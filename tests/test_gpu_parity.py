@@ -208,6 +208,105 @@ def test_local_second_best(engine):
     check(engine, rand_batch(22, 600, 30, 150, 30, 200), algo=G.LOCAL, second_best=1)
 
 
+def _with_env(name, on):
+    if on:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = "0"
+
+
+def test_local16_plan():
+    p = lambda **kw: G.make_params(algo=G.LOCAL, second_best=1, **kw)
+    assert G.describe_plan(p(), 150, 150) == "local16_second"
+    assert G.describe_plan(p(n_penalty=-2), 150, 150) == "local16_second"
+    # WITH_START / traceback, bytes outside [0, 255], values past the key window: int32
+    assert G.describe_plan(p(start_pos=G.WITH_START), 150, 150) == "generic_local"
+    assert G.describe_plan(p(start_pos=G.WITH_TB), 150, 150) == "generic_local"
+    assert G.describe_plan(p(match=200, mismatch=60), 150, 150) == "generic_local"
+    assert G.describe_plan(p(match=5), 1000, 1000) == "generic_local"
+
+
+LOCAL16_SCORES = [{}, dict(match=2, mismatch=3, gap_open=5, gap_extend=2),
+                  dict(match=3, mismatch=1, gap_open=1, gap_extend=1, n_penalty=2),
+                  dict(match=1, mismatch=4, gap_open=6, gap_extend=1, n_penalty=-1),
+                  dict(match=2, mismatch=0, gap_open=0, gap_extend=0)]
+
+
+@pytest.mark.parametrize("config", [2, 4])
+@pytest.mark.parametrize("scores", LOCAL16_SCORES)
+def test_local16_second_best_configs(engine, config, scores):
+    # one tile geometry per batch: every lane carries two pairs; an odd count leaves the
+    # last lane one pair.  n_penalty=-1 scores pad cells +1: they lead both maxima
+    check(engine, G.Batch.synth(config, 3001, 0x5EED0100 + config), algo=G.LOCAL, second_best=1, **scores)
+
+
+def test_local16_pads_differ_per_half(engine):
+    rng = np.random.default_rng(191)
+    qs, ts = [], []
+    for _ in range(2000):
+        q = helpers.random_seq(rng, int(rng.integers(145, 153)))
+        t = (helpers.mutate(rng, q) + helpers.random_seq(rng, 60))[:int(rng.integers(177, 185))]
+        qs.append(q); ts.append(t)
+    b = G.Batch.from_pairs(qs, ts)
+    for kw in ({}, dict(n_penalty=-1), dict(n_penalty=3)):
+        check(engine, b, algo=G.LOCAL, second_best=1, **kw)
+
+
+@pytest.mark.parametrize("n", [4000, 9001])
+def test_local16_mixed_geometry(engine, n):
+    # n >= 4096 pairs slots of equal geometry by a counting sort; smaller batches decline
+    # the second pair of a mismatched lane to the int32 kernel
+    check(engine, rand_batch(195 + n, n, 1, 260, 1, 300), algo=G.LOCAL, second_best=1)
+
+
+def test_local16_n_bases_and_iupac(engine):
+    # N inside a target: N tables (packed); N in a query or another letter: the int32 kernel
+    rng = np.random.default_rng(197)
+    qs, ts = [], []
+    for i in range(3000):
+        q = bytearray(helpers.random_seq(rng, 150))
+        t = bytearray((helpers.mutate(rng, bytes(q)) + helpers.random_seq(rng, 40))[:182])
+        if i % 7 == 0:
+            q[int(rng.integers(0, 150))] = ord("N")
+        if i % 3 == 0:
+            for _ in range(3):
+                t[int(rng.integers(0, 182))] = ord("N")
+        if i % 11 == 0:
+            t[int(rng.integers(0, 182))] = b"RYa"[i % 3]
+        qs.append(bytes(q)); ts.append(bytes(t))
+    b = G.Batch.from_pairs(qs, ts)
+    for kw in ({}, dict(n_penalty=3), dict(n_penalty=-2)):
+        check(engine, b, algo=G.LOCAL, second_best=1, **kw)
+
+
+def test_local16_value_window_edge(engine):
+    # H up to match * 1,704 = 3,408 (the key limit is 3,455)
+    rng = np.random.default_rng(199)
+    qs, ts = [], []
+    for _ in range(64):
+        q = helpers.random_seq(rng, 1700)
+        qs.append(q)
+        ts.append(helpers.mutate(rng, q, sub=0.005, indel=0.0)[:1704])
+    b = G.Batch.from_pairs(qs, ts)
+    kw = dict(algo=G.LOCAL, second_best=1, match=2, mismatch=3, gap_open=5, gap_extend=2)
+    assert G.describe_plan(G.make_params(**kw), 1700, 1704) == "local16_second"
+    check(engine, b, **kw)
+
+
+def test_local16_equals_int32_kernel(engine):
+    b = G.Batch.synth(2, 20000, 0x5EED0002)
+    p = G.make_params(algo=G.LOCAL, second_best=1)
+    r16 = engine.align_host(b, p)
+    try:
+        _with_env("GASALX_LOCAL16", False)
+        assert G.describe_plan(p, 150, 150) == "generic_local"
+        r32 = engine.align_host(b, p)
+    finally:
+        _with_env("GASALX_LOCAL16", True)
+    for f in ("score", "q_end", "t_end", "score2", "q_end2", "t_end2"):
+        assert np.array_equal(r16[f], r32[f]), f
+
+
 # ---------------------------------------------------------------- global ----
 @pytest.mark.parametrize("qr,tr", [((1, 30), (1, 30)), ((290, 310), (290, 310)), ((300, 300), (300, 300)),
                                    ((100, 1000), (100, 1000))])
