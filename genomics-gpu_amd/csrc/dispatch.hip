@@ -618,7 +618,8 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                     HIPCHK(ws.misc.reserve(n));
                     HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
                     D.todo = ws.misc.as<uint8_t>();
-                    HIPCHK(ws.aux.reserve((size_t)q8 * D.n_lanes * 8 + 64));
+                    D.rows_cap = q8;
+                    HIPCHK(ws.aux.reserve((size_t)q8 * ((D.n_lanes + 63) / 64) * 64 * 8 + 64));
                     D.rows = ws.aux.as<uint2>();
                     {
                         const int rc = geometry_perm(ws, b, shape, n, st, &D.perm);

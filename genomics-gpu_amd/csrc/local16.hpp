@@ -39,8 +39,8 @@ struct Local16Args {
     const uint32_t *perm;              // slot -> pair (NULL: identity)
     int32_t *score, *qend, *tend, *score2, *qend2, *tend2;
     uint8_t *todo;
-    uint2 *rows;                       // [row][lane]: (H, E) of both halves
-    uint32_t n, n_lanes;
+    uint2 *rows;                       // [wave][row][64 lanes]: (H, E) of both halves
+    uint32_t n, n_lanes, rows_cap;     // rows_cap: rows per wave (padded query length)
     int32_t a, b, oe, e, nval, sn;     // sn: the N score (0, or -N_PENALTY)
     uint32_t k, base;                  // table offset, stored value of 0
 };
@@ -81,9 +81,8 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
     const uint32_t BYTE_N = (uint32_t)(A.sn + (int32_t)A.k), SNK = BYTE_N * 0x10001u;
     // maxHH in key units with column bits 0: (Q - B)*8 + 0x400
     const uint32_t QK = ((uint32_t)(0x400 - 8 * (int32_t)A.base) & 0xFFFFu) * 0x10001u;
-    uint2 *rows = A.rows + lane;
-    const size_t rs = A.n_lanes;
-    for (uint32_t r = 0; r < QR * 8; ++r) rows[r * rs] = make_uint2(BB, BB);
+    // row buffer [wave][row][64 lanes]: the 8 rows of a tile at immediate offsets
+    uint2 *rw = A.rows + (size_t)(lane >> 6) * A.rows_cap * 64 + (lane & 63);
     uint32_t KC[8];
 #pragma unroll
     for (int m = 0; m < 8; ++m) KC[m] = ((uint32_t)(7 - m + 0x400 - 8 * (int32_t)A.base) & 0xFFFFu) * 0x10001u;
@@ -100,10 +99,8 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
     uint32_t Q = BB, x2 = 0;                         // running maximum (stored), maxXY_x_second
     uint32_t T0[8], T1[8], f[8], p[8];
     // one row of the strip; PAD: the row may be a pad row of either half (last tile)
-    auto row = [&](uint32_t r, uint32_t sel, uint32_t padm, uint32_t ss, auto pad_t) {
+    auto row = [&](uint32_t rr, uint2 he, uint2 *dst, uint32_t sel, uint32_t padm, auto pad_t) {
         constexpr bool PAD = decltype(pad_t)::value;
-        const uint32_t rr = r * 0x10001u;
-        const uint2 he = rows[r * rs];
         uint32_t left = he.x, e = he.y;   // H, E at the previous strip's last column
         uint32_t key[8], acc2 = 0u;
 #pragma unroll
@@ -122,7 +119,7 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
             p[m] = left;
             left = H;
         }
-        rows[r * rs] = make_uint2(left, e);
+        *dst = make_uint2(left, e);
         // first maximum: the row's largest key when its H is strictly higher
         const uint32_t m1 = pk_max3(key[0], key[1], key[2]), m2 = pk_max3(key[3], key[4], key[5]);
         const uint32_t rk = pk_max3(pk_max3(key[6], key[7], m1), m2, m2);
@@ -130,7 +127,6 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
         const uint32_t msk = l16_nz_mask(pk_subnb(t, b1.b7));
         b1.key = (b1.key & ~msk) | (rk & msk);
         b1.row = (b1.row & ~msk) | (rr & msk);
-        strip1 = (strip1 & ~msk) | (ss & msk);
         b1.b7 = t | 0x00070007u;
         // x2 = (prev_maxHH_second < maxHH) ? r : x2 with prev_maxHH_second = max2 before
         // this row (max2 only grows): max2 < maxHH iff max2*8 + 7 < maxHH*8 in key units
@@ -138,11 +134,16 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
         x2 = (x2 & ~xm) | (rr & xm);
         // second best: the row's largest candidate when strictly above max2
         const uint32_t t2 = pk_max_u16(acc2, b27);
-        const uint32_t msk2 = l16_nz_mask(pk_subnb(t2, b27));
-        k2 = (k2 & ~msk2) | (acc2 & msk2);
-        strip2 = (strip2 & ~msk2) | (ss & msk2);
+        k2 = pk_max_u16(k2, acc2 & l16_nz_mask(pk_subnb(t2, b27)));
         b27 = t2 | 0x00070007u;
     };
+    // tiles in strip-major order, the next tile's row buffer entries and query words
+    // loaded while this one computes (strip 0 starts from (0, 0) without loads; a
+    // one-tile query (QR == 1) reloads its rows after storing them)
+    uint2 nx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) nx[k] = make_uint2(BB, BB);
+    uint32_t nqa = qwa[0], nqb = qwb[0];
     for (uint32_t i = 0; i < TR; ++i) {
         // substitution tables of the strip, byte l = s(l, t) + K; pad and N columns: the N score
         const uint32_t ga = twa[i], gb = twb[i];
@@ -157,25 +158,48 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
             T1[m] = nb ? BYTE_N * 0x01010101u : BYTE_X * 0x01010101u + ((BYTE_M - BYTE_X) << (8 * ((cb >> 1) & 3u)));
             f[m] = BB; p[m] = BB;
         }
+        const uint32_t key0 = b1.key, k20 = k2;
+        for (uint32_t j = 0; j < QR; ++j) {
+            uint2 cu[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cu[k] = nx[k];
+            const uint32_t qa = nqa, qb = nqb;
+            const uint32_t nj = j + 1 < QR ? j + 1 : 0;
+            // the next tile is in strip 0 (its rows start at 0), in a later strip with
+            // QR > 1 (prefetch) or the same tile of the next strip (QR == 1, below)
+            const bool later = j + 1 == QR ? i + 1 < TR : i > 0;
+            uint2 *rb = rw + (size_t)j * 8 * 64;
+            if (later && QR > 1) {
+                const uint2 *nb = rw + (size_t)nj * 8 * 64;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) nx[k] = nb[k * 64];
+            }
+            if (nj != j) { nqa = qwa[nj]; nqb = qwb[nj]; }
+            const uint32_t la = (qa >> 1) & 0x33333333u, lb = ((qb >> 1) & 0x33333333u) + 0x44444444u;
+            if (j + 1 < QR) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t sel = ((la >> (28 - 4 * k)) & 15u) | (((lb >> (28 - 4 * k)) & 15u) << 16) | 0x0C000C00u;
+                    row((j * 8 + k) * 0x10001u, cu[k], rb + k * 64, sel, 0u, std::false_type{});
+                }
+            } else {   // the last tile: pad rows of either half score the N score
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t sel = ((la >> (28 - 4 * k)) & 15u) | (((lb >> (28 - 4 * k)) & 15u) << 16) | 0x0C000C00u;
+                    const uint32_t padm = ((uint32_t)k >= kpa ? 0x0000FFFFu : 0u) | ((uint32_t)k >= kpb ? 0xFFFF0000u : 0u);
+                    row((j * 8 + k) * 0x10001u, cu[k], rb + k * 64, sel, padm, std::true_type{});
+                }
+            }
+            if (QR == 1 && i + 1 < TR) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) nx[k] = rb[k * 64];
+            }
+        }
+        // strips of the maxima: the keys only grow, so a changed key was set in this strip
         const uint32_t ss = i * 0x10001u;
-        for (uint32_t j = 0; j + 1 < QR; ++j) {
-            const uint32_t la = (qwa[j] >> 1) & 0x33333333u, lb = ((qwb[j] >> 1) & 0x33333333u) + 0x44444444u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t sel = ((la >> (28 - 4 * k)) & 15u) | (((lb >> (28 - 4 * k)) & 15u) << 16) | 0x0C000C00u;
-                row(j * 8 + k, sel, 0u, ss, std::false_type{});
-            }
-        }
-        {   // the last tile: pad rows of either half score the N score
-            const uint32_t j = QR - 1;
-            const uint32_t la = (qwa[j] >> 1) & 0x33333333u, lb = ((qwb[j] >> 1) & 0x33333333u) + 0x44444444u;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t sel = ((la >> (28 - 4 * k)) & 15u) | (((lb >> (28 - 4 * k)) & 15u) << 16) | 0x0C000C00u;
-                const uint32_t padm = ((uint32_t)k >= kpa ? 0x0000FFFFu : 0u) | ((uint32_t)k >= kpb ? 0xFFFF0000u : 0u);
-                row(j * 8 + k, sel, padm, ss, std::true_type{});
-            }
-        }
+        const uint32_t c1 = l16_nz_mask(b1.key - key0), c2 = l16_nz_mask(k2 - k20);
+        strip1 = (strip1 & ~c1) | (ss & c1);
+        strip2 = (strip2 & ~c2) | (ss & c2);
     }
     auto out = [&](uint32_t pair, uint32_t half, bool ok) {
         const uint32_t sh = 16 * half;
