@@ -625,7 +625,8 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                         const int rc = geometry_perm(ws, b, shape, n, st, &D.perm);
                         if (rc) return rc;
                     }
-                    local2nd16_kernel<<<grid_for(D.n_lanes, 256), 256, 0, st>>>(D);
+                    // 3 waves per SIMD (162 VGPRs): 2 waves 2 % and 4 waves (spills) 5-15 % slower
+                    local2nd16_kernel<3><<<grid_for(D.n_lanes, 256), 256, 0, st>>>(D);
                     HIPCHK(hipGetLastError());
                     A.todo = D.todo;
                 }

@@ -58,7 +58,8 @@ __device__ __forceinline__ uint32_t l16_satsub(uint32_t x, uint32_t y) {
     return d;
 }
 
-__global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
+template <int WAVES>
+__global__ __launch_bounds__(256, WAVES) void local2nd16_kernel(Local16Args A) {
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= A.n_lanes) return;
     const uint32_t s0 = 2 * lane, s1 = s0 + 1;
@@ -93,8 +94,8 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
         ok_b &= band_word_ok(qwb[j], qlb - 8 * j);
     }
     const uint32_t kpa = qla - 8 * (QR - 1), kpb = qlb - 8 * (QR - 1);
-    BandBest b1 = {0x04070407u, 0x04070407u, 0u};
-    uint32_t k2 = 0x04070407u, b27 = 0x04070407u;   // second best key, its key | 7
+    BandBest b1 = {0x04070407u, 0u, 0u};             // first maximum (key, row)
+    uint32_t k2 = 0x04070407u;                       // second best key
     uint32_t strip1 = 0, strip2 = 0;                 // strip of b1 / of k2 (16 bits per half)
     uint32_t Q = BB, x2 = 0;                         // running maximum (stored), maxXY_x_second
     uint32_t T0[8], T1[8], f[8], p[8];
@@ -102,7 +103,8 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
     auto row = [&](uint32_t rr, uint2 he, uint2 *dst, uint32_t sel, uint32_t padm, auto pad_t) {
         constexpr bool PAD = decltype(pad_t)::value;
         uint32_t left = he.x, e = he.y;   // H, E at the previous strip's last column
-        uint32_t key[8], acc2 = 0u;
+        const uint32_t Q0 = Q;
+        uint32_t key[8], cand[8];
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             uint32_t v = __builtin_amdgcn_perm(T1[m], T0[m], sel);
@@ -113,29 +115,29 @@ __global__ __launch_bounds__(256) void local2nd16_kernel(Local16Args A) {
             f[m] = pk_max3(toe, pk_subnb(f[m], EXT), BB);
             e = pk_max3(toe, pk_subnb(e, EXT), BB);
             key[m] = band_key(H, KC[m]);
-            // second best: the cell counts iff H < Q, the running maximum before it
-            acc2 = pk_max_u16(acc2, key[m] & l16_nz_mask(l16_satsub(Q, H)));
+            // second best: the cell counts iff H < the running maximum after it
             Q = pk_max_u16(Q, H);
+            cand[m] = key[m] & l16_nz_mask(pk_subnb(Q, H));
             p[m] = left;
             left = H;
         }
         *dst = make_uint2(left, e);
-        // first maximum: the row's largest key when its H is strictly higher
+        // first maximum: the row's largest key when the row raised the running maximum
         const uint32_t m1 = pk_max3(key[0], key[1], key[2]), m2 = pk_max3(key[3], key[4], key[5]);
         const uint32_t rk = pk_max3(pk_max3(key[6], key[7], m1), m2, m2);
-        const uint32_t t = pk_max_u16(rk, b1.b7);
-        const uint32_t msk = l16_nz_mask(pk_subnb(t, b1.b7));
+        const uint32_t msk = l16_nz_mask(pk_subnb(Q, Q0));
         b1.key = (b1.key & ~msk) | (rk & msk);
         b1.row = (b1.row & ~msk) | (rr & msk);
-        b1.b7 = t | 0x00070007u;
         // x2 = (prev_maxHH_second < maxHH) ? r : x2 with prev_maxHH_second = max2 before
         // this row (max2 only grows): max2 < maxHH iff max2*8 + 7 < maxHH*8 in key units
+        const uint32_t b27 = k2 | 0x00070007u;
         const uint32_t xm = l16_nz_mask(l16_satsub(band_key(Q, QK), b27));
         x2 = (x2 & ~xm) | (rr & xm);
-        // second best: the row's largest candidate when strictly above max2
-        const uint32_t t2 = pk_max_u16(acc2, b27);
-        k2 = pk_max_u16(k2, acc2 & l16_nz_mask(pk_subnb(t2, b27)));
-        b27 = t2 | 0x00070007u;
+        // second best: the row's largest candidate when its H is strictly above max2
+        const uint32_t c1 = pk_max3(cand[0], cand[1], cand[2]), c2 = pk_max3(cand[3], cand[4], cand[5]);
+        const uint32_t acc2 = pk_max3(pk_max3(cand[6], cand[7], c1), c2, c2);
+        const uint32_t msk2 = l16_nz_mask(l16_satsub(acc2, b27));
+        k2 = (k2 & ~msk2) | (acc2 & msk2);
     };
     // tiles in strip-major order, the next tile's row buffer entries and query words
     // loaded while this one computes (strip 0 starts from (0, 0) without loads; a
