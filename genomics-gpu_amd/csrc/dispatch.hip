@@ -596,7 +596,28 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                 HIPCHK(ws.misc.reserve(n));
                 HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
                 todo = ws.misc.as<uint8_t>();
-                gen_ksw_kernel<0><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
+                // level 0 with the entries in LDS when two blocks of >= 64 threads fit
+                // a CU, for batches of up to 4 waves per SIMD: LDS then holds 2 waves
+                // per SIMD, and larger batches run faster on the global array with its
+                // higher occupancy (200 K config-2 pairs: 806 -> 890 GCUPS; 1 M: 1,320
+                // global, 1,146 LDS).  GASALX_KSW_LDS=0/1 forces either (A/B)
+                const char *kl = std::getenv("GASALX_KSW_LDS");
+                const bool lds_on = kl ? std::atoi(kl) != 0 : n <= 4u * 1024u * 64u;
+                uint32_t tpb = 0;
+                size_t lds = 0;
+                if (lds_on)
+                    for (uint32_t t : {256u, 128u, 64u}) {
+                        lds = (size_t)t * (shape.max_q + 2) * 2;
+                        if (2 * lds <= 160 * 1024) { tpb = t; break; }
+                    }
+                if (tpb) {
+                    if (lds > 64 * 1024)
+                        HIPCHK(hipFuncSetAttribute((const void *)&gen_ksw_kernel<0, true>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    gen_ksw_kernel<0, true><<<grid_for(n, tpb), tpb, lds, st>>>(A, ws.rows_h.p, todo);
+                } else {
+                    gen_ksw_kernel<0><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
+                }
                 gen_ksw_kernel<1><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);
             }
             gen_ksw_kernel<2><<<grid_for(n, 256), 256, 0, st>>>(A, ws.rows_h.p, todo);

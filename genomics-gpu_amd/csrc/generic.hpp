@@ -425,8 +425,16 @@ __device__ __forceinline__ int ksw_wave_max(int v) {
 // 32 bits, 2 = int2 (both values are >= 0 and at most h0 + match * min(qlen, tlen)).
 // The loop is bound by its entry traffic, so narrower entries run faster; a pair whose
 // bound does not fit its level is flagged (todo = level + 1) for the next instance.
-template <int LEVEL>
+//
+// INLDS (level 0 only): the pair's entries live in LDS, [column][thread] uint16 of
+// the block (2 * blockDim * (max qlen + 2) bytes, dispatch.hip sizes the block so
+// two fit a CU), instead of the [column][pair] global array: no lockstep column
+// start is needed (any mix of columns is bank-conflict free: a thread's bank is
+// fixed by its index) and the row's entries never leave the CU.
+template <int LEVEL, bool INLDS = false>
 __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint8_t *todo) {
+    static_assert(!INLDS || LEVEL == 0, "LDS entries are the 8-bit level");
+    extern __shared__ __attribute__((aligned(16))) uint16_t ksw_lds[];
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     // lanes past n, and pairs of the other instance, run the wave's row loop without work
     bool live = tid < A.n && (todo ? todo[tid] == LEVEL : LEVEL == 2);
@@ -445,13 +453,15 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint
     uint32_t *ehn = reinterpret_cast<uint32_t *>(ehv);
     uint16_t *ehb = reinterpret_cast<uint16_t *>(ehv);
     auto put = [&](int j, int h, int e) {
-        if (LEVEL == 0) ehb[(size_t)j * A.n + tid] = (uint16_t)((uint32_t)h | ((uint32_t)e << 8));
+        if (INLDS) ksw_lds[(uint32_t)j * blockDim.x + threadIdx.x] = (uint16_t)((uint32_t)h | ((uint32_t)e << 8));
+        else if (LEVEL == 0) ehb[(size_t)j * A.n + tid] = (uint16_t)((uint32_t)h | ((uint32_t)e << 8));
         else if (LEVEL == 1) ehn[(size_t)j * A.n + tid] = (uint32_t)h | ((uint32_t)e << 16);
         else ehw[(size_t)j * A.n + tid] = make_int2(h, e);
     };
     auto get = [&](int j) {
         if (LEVEL == 0) {
-            const uint32_t v = ehb[(size_t)j * A.n + tid];
+            const uint32_t v = INLDS ? (uint32_t)ksw_lds[(uint32_t)j * blockDim.x + threadIdx.x]
+                                     : (uint32_t)ehb[(size_t)j * A.n + tid];
             return make_int2((int)(v & 0xFFu), (int)(v >> 8));
         }
         if (LEVEL == 1) {
@@ -481,7 +491,7 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint
             if (i < (int)tlen) gpac = tw[i >> 3];
         }
         const bool act = i < (int)tlen && !skip;
-        const int jlo = ksw_wave_min(act ? beg : 0x7FFFFFFF);
+        const int jlo = INLDS ? beg : ksw_wave_min(act ? beg : 0x7FFFFFFF);
         if (!act) continue;
         const uint32_t gbase = (gpac >> (28 - 4 * (i & 7))) & 0x0F;
         int t, f = 0, h1, m = 0, mj = -1;

@@ -553,6 +553,18 @@ def test_ksw_trimming(engine, lens, seeds):
     check(engine, b, seed=seed, algo=G.KSW, match=2, mismatch=3, gap_open=5, gap_extend=2)
 
 
+@pytest.mark.parametrize("lds", ["0", "1"])
+@pytest.mark.parametrize("lens", [(100, 150), (400, 600), (700, 800)])
+def test_ksw_entry_storage(engine, monkeypatch, lds, lens):
+    # 8-bit level entries in LDS (block of 256 / 128 / 64 threads by query length; none
+    # fits past ~630 bp) or in the global [column][pair] array: both against the oracle
+    monkeypatch.setenv("GASALX_KSW_LDS", lds)
+    rng = np.random.default_rng(lens[0] + int(lds))
+    b = rand_batch(int(rng.integers(1 << 16)), 700, *lens, *lens, related=0.8)
+    seed = rng.integers(0, 40, b.n).astype(np.uint32)
+    check(engine, b, seed=seed, algo=G.KSW)
+
+
 # ------------------------------------------------ reverse / complement ----
 @pytest.mark.parametrize("algo", [G.LOCAL, G.GLOBAL, G.SEMI_GLOBAL])
 def test_reverse_complement_ops(engine, algo):
