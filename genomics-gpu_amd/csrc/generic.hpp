@@ -423,8 +423,9 @@ __device__ __forceinline__ int ksw_wave_max(int v) {
 
 // The entry width is a level: 0 = (h, e) as two uint8 in 16 bits, 1 = two uint16 in
 // 32 bits, 2 = int2 (both values are >= 0 and at most h0 + match * min(qlen, tlen)).
-// The loop is bound by its entry traffic, so narrower entries run faster; a pair whose
-// bound does not fit its level is flagged (todo = level + 1) for the next instance.
+// Narrower entries cut the loop's traffic (603 -> 808 GCUPS); a pair whose bound does
+// not fit its level is flagged (todo = level + 1) for the next instance.  The loop is
+// then bound by its VALU work (profiles/r02_ksw_lds_ab.md).
 //
 // INLDS (level 0 only): the pair's entries live in LDS, [column][thread] uint16 of
 // the block (2 * blockDim * (max qlen + 2) bytes, dispatch.hip sizes the block so
@@ -494,7 +495,12 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint
         const int jlo = INLDS ? beg : ksw_wave_min(act ? beg : 0x7FFFFFFF);
         if (!act) continue;
         const uint32_t gbase = (gpac >> (28 - 4 * (i & 7))) & 0x0F;
-        int t, f = 0, h1, m = 0, mj = -1;
+        // substitution scores of this row (g_sub_local): N in the target row scores every
+        // cell N; otherwise match / mismatch, or N for an N in the query
+        const int32_t nsc = A.has_npen ? -A.npen : 0;
+        const bool gN = (int32_t)gbase == A.nval;
+        const int32_t sc_eq = gN ? nsc : A.a, sc_ne = gN ? nsc : -A.b;
+        int f = 0, h1, m = 0, mj = -1;
         if (beg == 0) {
             h1 = (int32_t)(h0 - (uint32_t)(o_del + e_del * (i + 1)));
             if (h1 < 0) h1 = 0;
@@ -506,20 +512,19 @@ __global__ __launch_bounds__(256) void gen_ksw_kernel(GenArgs A, void *ehv, uint
             if (j < beg) continue;
             const uint32_t rbase = (rpac >> (28 - 4 * (j & 7))) & 0x0F;
             const int2 v = get(j);
-            int h, M = v.x, e = v.y;
+            int M = v.x, e = v.y;
             const int hs = h1;           // H(i, j-1), stored for the next row
-            M = M ? M + g_sub_local(A, rbase, gbase) : 0;
-            h = M > e ? M : e;
-            h = h > f ? h : f;
+            int sc = rbase == gbase ? sc_eq : sc_ne;
+            sc = (int32_t)rbase == A.nval ? nsc : sc;
+            M = M ? M + sc : 0;
+            const int h = max(max(M, e), f);
             h1 = h;
             mj = m > h ? mj : j;
             m = m > h ? m : h;
-            t = M - oe_del; t = t > 0 ? t : 0;
-            e -= e_del; e = e > t ? e : t;
+            e = max(max(e - e_del, M - oe_del), 0);   // (:122-131) t = max(M - oe, 0); e = max(e - e, t)
             put(j, hs, e);
             if ((hs | e) != 0) { first = min(first, j); last = j; }   // h, e >= 0
-            t = M - oe_ins; t = t > 0 ? t : 0;
-            f -= e_ins; f = f > t ? f : t;
+            f = max(max(f - e_ins, M - oe_ins), 0);
         }
         put(end, h1, 0);
         if (h1 != 0) { first = min(first, end); last = end; }
