@@ -73,6 +73,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
+#ifndef GX_WF16_CAPTURE_TREE
+#define GX_WF16_CAPTURE_TREE 0   // GLOBAL kernels: branch-free score / start-cell capture
+#endif
 #ifndef GX_WF16_TB_INPLACE
 #define GX_WF16_TB_INPLACE 0
 #endif
@@ -570,6 +573,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         uint32_t kq_lane[2], kq[2], kp_lane[2], kp[2];
         bool fixable[2];
         int32_t score[2] = {0, 0}, fixv[2] = {0, 0};
+        uint32_t capq[2] = {0, 0}, capp[2] = {0, 0};   // GX_WF16_CAPTURE_TREE: the captured registers
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             kq_lane[h] = (xl[h] - 1) / R;
@@ -603,6 +607,29 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                       EXTD, NN, j);
                 else
                     step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, OED, EXTD, NN);
+#if GX_WF16_CAPTURE_TREE
+                // branch-free capture: every lane picks one register by a select tree
+                // over the bits of its index (score: row xl - 1 at column yl - 1; fix:
+                // row xl at column yl); a capture inside a per-lane branch holds ~45
+                // more VGPRs
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const bool late = GTB && cc >= (int32_t)yl[h];
+                    const uint32_t idx = late ? kp[h] : kq[h];
+                    uint32_t t[R];
+#pragma unroll
+                    for (int k = 0; k < R; ++k) t[k] = Hout[k];
+#pragma unroll
+                    for (int bb = 1; bb < R; bb <<= 1) {
+                        const bool bit = (idx & (uint32_t)bb) != 0;
+#pragma unroll
+                        for (int k = 0; k + bb < R; k += 2 * bb) t[k] = bit ? t[k + bb] : t[k];
+                    }
+                    capq[h] = cc == (int32_t)yl[h] - 1 ? t[0] : capq[h];
+                    if (GTB) capp[h] = cc == (int32_t)yl[h] ? t[0] : capp[h];
+                }
+            }
+#else
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
@@ -619,6 +646,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     }
                 }
             }
+#endif
             prevRecvH = recvH;
             recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
             recvF = (uint32_t)shr_lane((int32_t)f);
@@ -661,6 +689,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     }
                 }
             }
+#if GX_WF16_CAPTURE_TREE
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                fixv[h] = (int32_t)((capp[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
+#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (fixable[h] && lg == kp_lane[h]) A.tbfix[pr[h]] = fixv[h];
@@ -670,6 +703,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 half_step(c + 1, 1, HB, HA);
             }
         }
+#if GX_WF16_CAPTURE_TREE
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            score[h] = (int32_t)((capq[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h] - 2);
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             if (valid[h] && lg == kq_lane[h]) A.score[pr[h]] = score[h];
