@@ -759,7 +759,9 @@ static int pairhmm_launch(HmmArgs A, bool quals, int G, uint32_t slot0, uint32_t
     A.n = slot1;
     A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
     HmmFn fn = quals ? hmm_lookup<true>(G) : hmm_lookup<false>(G);
-    const size_t lds = (size_t)4 * (64 / G) * A.lds_stride;
+    // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
+    // 8 rows x 64 lanes x 4 bytes
+    const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * 8 * 64 * 4;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
     if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);

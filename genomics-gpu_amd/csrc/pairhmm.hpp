@@ -4,12 +4,18 @@
 // (identical arithmetic in Intra-task/.../improved_warp_based.cu:91-172).
 // G lanes per pair, RR read rows per lane; haplotype bytes staged in LDS; the
 // (M, I, D) of a lane's bottom row cross to the next lane with DPP wave_shr:1.
+// The match/mismatch prior of a cell, (hb == rb) ? 1 - Qm : Qm / 3, is read from a
+// per-lane LDS table indexed by the haplotype base (two ds_read_b128 per column
+// for 8 rows, instead of 8 compares + 8 selects: 4,488 -> ~4,950 GCUPS on config
+// 5, profiles/r02_pairhmm_ab.md); blocks with bases other than A/C/G/T compare.
 // Every rounding step is the reference's: products and sums are separate
 // roundings (__fmul_rn/__fadd_rn), the three FMAs are the reference's
 // __fmaf_rn sites; this file is compiled with -ffp-contract=off.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 namespace gx {
 
@@ -36,8 +42,12 @@ struct HmmArgs {
 __device__ __forceinline__ float shr_lane_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
 }
+__device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
+#ifndef GX_HMM_WAVES
+#define GX_HMM_WAVES 3   // waves per SIMD the register allocator must allow
+#endif
 template <int G, int RR, bool QUALS = false>
-__global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
+__global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int P = 64 / G;
     const float c0 = 1.329228e+36f, c09 = 0.9f, c01 = 0.1f;     // tile_1.cu:228-233
@@ -49,10 +59,11 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
     uint32_t R = 0, H = 0, ro = 0, ho = 0;
     if (valid) { R = A.rlen[pair]; H = A.hlen[pair]; ro = A.roff[pair]; ho = A.hoff[pair]; }
 
-    // stage haplotypes
+    // stage haplotypes; note whether the block holds a base other than A/C/G/T
     const uint32_t stride = A.lds_stride;
     uint8_t *wl = lds + (size_t)wave * P * stride;
     const uint32_t words = stride >> 2;
+    bool other = false;
     for (uint32_t base = 0; base < P * words; base += 64) {
         const uint32_t idx = base + lane;
         const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
@@ -60,11 +71,14 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
         if (idx < P * words) {
             uint32_t v = 0;
             for (int b = 0; b < 4; ++b)
-                if (4 * w + b < pH) v |= (uint32_t)A.haps[pho + 4 * w + b] << (8 * b);
+                if (4 * w + b < pH) {
+                    const uint32_t hb = A.haps[pho + 4 * w + b];
+                    other |= !acgt(hb);
+                    v |= hb << (8 * b);
+                }
             reinterpret_cast<uint32_t *>(wl + ps * stride)[w] = v;
         }
     }
-    __syncthreads();
     const uint8_t *hap = wl + slot * stride;
 
     // the lane's read rows and their parameters (tile_1.cu:89-118).  Rows are
@@ -95,6 +109,7 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
             }
         }
         rb[k] = in ? A.reads[ro + i] : 0x100u;
+        other |= in && !acgt(rb[k]);
         qm1[k] = in ? __fsub_rn(1.0f, q) : 0.f;     // Qm_1 = constant[1] - Qm
         qm3[k] = in ? __fdiv_rn(q, 3.0f) : 0.f;     // fdividef(Qm, 3) (<= 2 ulp in the reference)
         de[k] = d;
@@ -105,60 +120,125 @@ __global__ __launch_bounds__(256) void pairhmm_kernel(HmmArgs A) {
         Dk[k] = in ? 0.f : D0;
         MM[k] = i == 0 ? __fmul_rn(c09, D0) : 0.f;                     // first row's MMID (:117)
     }
-
-    uint32_t hmax = H;
+    // A/C/G/T blocks (every real input so far): the prior of each row for each
+    // haplotype base, (hb == rb) ? 1 - Qm : Qm / 3, is tabulated once per lane in LDS,
+    // so a column costs two 16-byte LDS reads instead of RR compares and selects.
+    // Layout: [wave][code][quad][lane] float4, code = (base >> 1) & 3, so that the
+    // lanes of one read are 16 consecutive bytes whatever their codes.
+    const bool tab = !__syncthreads_or(other);
+    constexpr int NQ = RR / 4;
+    const uint32_t tbl_off = (4u * P * stride + 15u) & ~15u;
+    const uint8_t *tb = lds + tbl_off + (size_t)wave * (4 * NQ * 64 * 16) + lane * 16;
+    if (tab) {
+        float4 *tw = reinterpret_cast<float4 *>(lds + tbl_off + (size_t)wave * (4 * NQ * 64 * 16) + lane * 16);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, m));
-    const uint32_t nsteps = hmax + G - 1;
+        for (int cd = 0; cd < 4; ++cd) {
+            const uint32_t base = "ACTG"[cd];
+#pragma unroll
+            for (int qd = 0; qd < NQ; ++qd) {
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = rb[4 * qd + u] == base ? qm1[4 * qd + u] : qm3[4 * qd + u];
+                tw[(cd * NQ + qd) * 64] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+    }
+    // rows' priors for haplotype byte hb: from the table (tab) or by compare
+    auto tload = [&](uint32_t hb, float (&aa)[RR]) {
+        const float4 *p = reinterpret_cast<const float4 *>(tb + (hb & 6u) * (NQ * 512u));   // code * NQ * 1 KB
+#pragma unroll
+        for (int qd = 0; qd < NQ; ++qd) {
+            const float4 x = p[qd * 64];
+            aa[4 * qd] = x.x; aa[4 * qd + 1] = x.y; aa[4 * qd + 2] = x.z; aa[4 * qd + 3] = x.w;
+        }
+    };
+    auto cload = [&](uint32_t hb, float (&aa)[RR]) {
+#pragma unroll
+        for (int k = 0; k < RR; ++k) aa[k] = (hb == rb[k]) ? qm1[k] : qm3[k];
+    };
+
+    // the sweep, instantiated once per prior source so that the compare path's
+    // registers (rb, qm1, qm3) are dead in the table path
     const bool bottom = lg == G - 1;
     float acc = 0.f;
-    float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
+    auto sweep = [&](auto tabc) {
+        constexpr bool TABP = decltype(tabc)::value;
+        uint32_t hmax = H;
+    #pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, m));
+        const uint32_t nsteps = hmax + G - 1;
+        float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
 
-    // one column j of the lane's rows; (MU, IU, DU) in = row r0-1, out = the lane's bottom row
-    auto column = [&](uint32_t hb, float &MU, float &IU, float &DU) {
-#pragma unroll
-        for (int k = 0; k < RR; ++k) {
-            const float MID = __fadd_rn(IU, DU);                   // :149-162
-            const float DDM = __fmul_rn(Mk[k], xi[k]);
-            const float IIMI = __fmul_rn(IU, c01);
-            const float aa = (hb == rb[k]) ? qm1[k] : qm3[k];
-            const float MIIDD = __fmul_rn(c09, MID);
-            const float Mn = __fmul_rn(aa, MM[k]);
-            const float In = __fmaf_rn(MU, de[k], IIMI);
-            const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
-            MM[k] = __fmaf_rn(al[k], MU, MIIDD);
-            Mk[k] = Mn; Dk[k] = Dn;
-            MU = Mn; IU = In; DU = Dn;
-        }
-    };
-    auto checked_step = [&](uint32_t s) {
-        const int32_t j = (int32_t)s - (int32_t)lg;
-        float MU, IU, DU;
-        if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }                  // row -1: M=I=0, D=D0
-        else { MU = rM; IU = rI; DU = rD; }
-        if (valid && j >= 0 && (uint32_t)j < H) {
-            column(hap[j], MU, IU, DU);
-            if (bottom) acc = __fadd_rn(acc, __fadd_rn(MU, IU));       // row R-1, column j (:166-167)
-        }
-        rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
-    };
-    {
+        // one column j of the lane's rows; (MU, IU, DU) in = row r0-1, out = the lane's bottom row
+        auto column = [&](const float (&aa)[RR], float &MU, float &IU, float &DU) {
+    #pragma unroll
+            for (int k = 0; k < RR; ++k) {
+                const float MID = __fadd_rn(IU, DU);                   // :149-162
+                const float DDM = __fmul_rn(Mk[k], xi[k]);
+                const float IIMI = __fmul_rn(IU, c01);
+                const float MIIDD = __fmul_rn(c09, MID);
+                const float Mn = __fmul_rn(aa[k], MM[k]);
+                const float In = __fmaf_rn(MU, de[k], IIMI);
+                const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
+                MM[k] = __fmaf_rn(al[k], MU, MIIDD);
+                Mk[k] = Mn; Dk[k] = Dn;
+                MU = Mn; IU = In; DU = Dn;
+            }
+        };
+        auto checked_step = [&](uint32_t s) {
+            const int32_t j = (int32_t)s - (int32_t)lg;
+            float MU, IU, DU;
+            if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }                  // row -1: M=I=0, D=D0
+            else { MU = rM; IU = rI; DU = rD; }
+            if (valid && j >= 0 && (uint32_t)j < H) {
+                float aa[RR];
+                if constexpr (TABP) tload(hap[j], aa);
+                else cload(hap[j], aa);
+                column(aa, MU, IU, DU);
+                if (bottom) acc = __fadd_rn(acc, __fadd_rn(MU, IU));       // row R-1, column j (:166-167)
+            }
+            rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+        };
         // steps [G-1, hmin): every lane of the wave is inside its pair's columns, so
         // no activity test and no merge of state
-        uint32_t hmin = valid ? H : 0u;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) hmin = min(hmin, (uint32_t)__shfl_xor(hmin, m));
-        const uint32_t s1 = min((uint32_t)G - 1, nsteps), s2 = max(s1, hmin);
-        for (uint32_t s = 0; s < s1; ++s) checked_step(s);
-        for (uint32_t s = s1; s < hmin; ++s) {
+        auto steady = [&](const float (&aa)[RR]) {
             float MU = rM, IU = rI, DU = rD;
             if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }
-            column(hap[s - lg], MU, IU, DU);
-            acc = __fadd_rn(acc, __fadd_rn(MU, IU));                   // kept by the bottom lane only
+            column(aa, MU, IU, DU);
+            acc = __fadd_rn(acc, __fadd_rn(MU, IU));                       // kept by the bottom lane only
             rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+        };
+        {
+            uint32_t hmin = valid ? H : 0u;
+    #pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) hmin = min(hmin, (uint32_t)__shfl_xor(hmin, m));
+            const uint32_t s1 = min((uint32_t)G - 1, nsteps), s2 = max(s1, hmin);
+            for (uint32_t s = 0; s < s1; ++s) checked_step(s);
+            if constexpr (TABP) {
+                // table rows one step ahead, two register sets in turn (hap reads past a
+                // pair's columns stay inside the slot + table region and are not used)
+                float aaA[RR], aaB[RR];
+                uint32_t s = s1;
+                if (s < hmin) tload(hap[s - lg], aaA);
+                for (; s + 1 < hmin; s += 2) {
+                    tload(hap[s + 1 - lg], aaB);
+                    steady(aaA);
+                    tload(hap[s + 2 - lg], aaA);
+                    steady(aaB);
+                }
+                if (s < hmin) steady(aaA);
+            } else {
+                for (uint32_t s = s1; s < hmin; ++s) {
+                    float aa[RR];
+                    cload(hap[s - lg], aa);
+                    steady(aa);
+                }
+            }
+            for (uint32_t s = s2; s < nsteps; ++s) checked_step(s);
         }
-        for (uint32_t s = s2; s < nsteps; ++s) checked_step(s);
-    }
+    };
+    if (tab) sweep(std::true_type{});
+    else sweep(std::false_type{});
     if (valid && bottom) A.result[pair] = acc;
 }
 

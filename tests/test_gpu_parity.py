@@ -778,6 +778,36 @@ def test_pairhmm_edge_lengths(engine):
     np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
 
 
+def test_pairhmm_prior_table_vs_compare(engine):
+    # pairhmm.hpp: blocks whose bases are all A/C/G/T read the rows' priors from the
+    # per-lane LDS table, blocks holding any other byte compare per row.  The same pairs
+    # must give the same floats either way: pure A/C/G/T pairs alone (table), then each
+    # followed by a pair with N / other bytes (every block compares)
+    rng = np.random.default_rng(0xAB1E)
+    pure, odd = [], []
+    for i in range(96):
+        H = int(rng.integers(30, 500)) if i else 500
+        R = int(rng.integers(5, min(H, 250))) if i else 250
+        hap = helpers.random_seq(rng, H).decode()
+        read = helpers.random_seq(rng, R).decode() if i % 3 == 0 else (hap * 2)[:R]
+        q = dict(bq=rng.integers(5, 50, R), iq=rng.integers(10, 60, R), dq=rng.integers(10, 60, R))
+        pure.append(dict(read=read, hap=hap, **q))
+        oh = bytearray(hap.encode())
+        orr = bytearray(read.encode())
+        for j in rng.integers(0, H, 3):
+            oh[j] = b"NacgtX"[int(rng.integers(0, 6))]
+        orr[int(rng.integers(0, R))] = ord("N")
+        odd.append(dict(read=orr.decode(), hap=oh.decode(), **q))
+    mixed = [p for ab in zip(pure, odd) for p in ab]
+    a = _hmm_batch(pure)
+    gp = engine.pairhmm_host(*a)
+    gm = engine.pairhmm_host(*_hmm_batch(mixed))
+    assert np.array_equal(gp, gm[0::2])
+    np.testing.assert_allclose(gp, O.pairhmm(*a), rtol=1e-5)
+    m = _hmm_batch(mixed)
+    np.testing.assert_allclose(gm, O.pairhmm(*m), rtol=1e-5)
+
+
 def test_host_pipeline_pinned_cigar(engine):
     # a caller-owned page-locked CIGAR buffer (bench.py end_to_end "pinned_cigar") must
     # come back byte-identical to the library-allocated one, whatever it held before
