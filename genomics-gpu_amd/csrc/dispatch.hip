@@ -731,14 +731,14 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
 
 // ----------------------------------------------------------------------------
 using HmmFn = void (*)(HmmArgs);
-template <bool QUALS>
+template <bool QUALS, bool ABS>
 static HmmFn hmm_lookup(int G) {
     switch (G) {
-        case 4: return &pairhmm_kernel<4, 8, QUALS>;
-        case 8: return &pairhmm_kernel<8, 8, QUALS>;
-        case 16: return &pairhmm_kernel<16, 8, QUALS>;
-        case 32: return &pairhmm_kernel<32, 8, QUALS>;
-        case 64: return &pairhmm_kernel<64, 8, QUALS>;
+        case 4: return &pairhmm_kernel<4, 8, QUALS, ABS>;
+        case 8: return &pairhmm_kernel<8, 8, QUALS, ABS>;
+        case 16: return &pairhmm_kernel<16, 8, QUALS, ABS>;
+        case 32: return &pairhmm_kernel<32, 8, QUALS, ABS>;
+        case 64: return &pairhmm_kernel<64, 8, QUALS, ABS>;
         default: return nullptr;
     }
 }
@@ -751,14 +751,19 @@ int pairhmm_group(uint32_t max_r) {
 }
 
 // One launch over slots [slot0, slot1) of A (A.perm maps slots to pairs, or NULL).
-static int pairhmm_launch(HmmArgs A, bool quals, int G, uint32_t slot0, uint32_t slot1, uint32_t max_h,
+static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0, uint32_t slot1, uint32_t max_h,
                           hipStream_t st) {
+    const int G = pairhmm_group(max_r);
     if (slot1 <= slot0) return GASALX_OK;
     if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
     A.slot0 = slot0;
     A.n = slot1;
     A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
-    HmmFn fn = quals ? hmm_lookup<true>(G) : hmm_lookup<false>(G);
+    // reads shorter than the group's rows: the top lane's first row is virtual and
+    // absorbs the boundary (pairhmm.hpp ABS)
+    const bool absorb = (uint32_t)G * 8 > max_r;
+    HmmFn fn = quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
+                     : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G));
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
     // 8 rows x 64 lanes x 4 bytes
     const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * 8 * 64 * 4;
@@ -779,7 +784,7 @@ int pairhmm_device(Workspace &ws, const gasalx_hmm_batch &b, float *result, hipS
     A.qm = b.qm; A.delta = b.delta; A.xiksi = b.xiksi; A.alpha = b.alpha;
     A.haps = b.haps; A.hoff = b.hap_offsets; A.hlen = b.hap_lens;
     A.result = result;
-    return pairhmm_launch(A, false, pairhmm_group(max_r), 0, b.n_pairs, max_h, st);
+    return pairhmm_launch(A, false, max_r, 0, b.n_pairs, max_h, st);
 }
 
 int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *result, hipStream_t st,
@@ -794,9 +799,9 @@ int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *r
     A.haps = b.haps; A.hoff = b.hap_offsets; A.hlen = b.hap_lens;
     A.result = result;
     A.perm = perm;
-    if (!classes) return pairhmm_launch(A, true, pairhmm_group(max_r), 0, b.n_pairs, max_h, st);
+    if (!classes) return pairhmm_launch(A, true, max_r, 0, b.n_pairs, max_h, st);
     for (int c = 0; c < n_classes; c++) {
-        int rc = pairhmm_launch(A, true, pairhmm_group(classes[c].max_r), classes[c].slot0, classes[c].slot1,
+        int rc = pairhmm_launch(A, true, classes[c].max_r, classes[c].slot0, classes[c].slot1,
                                 classes[c].max_h, st);
         if (rc) return rc;
     }

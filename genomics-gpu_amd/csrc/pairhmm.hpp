@@ -39,6 +39,10 @@ struct HmmArgs {
     uint32_t slot0;
 };
 
+// lane 0 of the wave reads 0 (bound_ctrl); no old value to set up
+__device__ __forceinline__ float shr_lane_fb(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float shr_lane_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
 }
@@ -46,7 +50,7 @@ __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' |
 #ifndef GX_HMM_WAVES
 #define GX_HMM_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
-template <int G, int RR, bool QUALS = false>
+template <int G, int RR, bool QUALS = false, bool ABS = false>
 __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int P = 64 / G;
@@ -168,6 +172,11 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
         for (int m = 32; m >= 1; m >>= 1) hmax = max(hmax, (uint32_t)__shfl_xor(hmax, m));
         const uint32_t nsteps = hmax + G - 1;
         float rM = 0.f, rI = 0.f, rD = 0.f;    // bottom-row values of the lane above, this column
+        // ABS (every read of the launch shorter than G*RR rows, so row 0 of lane 0 is
+        // virtual): that row takes I x 0 instead of I x 0.1, and with prior, delta and
+        // alpha 0 and D decay 1 its outputs are (0, 0, D0) whatever finite (M, I, D)
+        // comes in, so the top lane needs no boundary select in the steady steps
+        const float c01_0 = (ABS && lg == 0) ? 0.f : c01;
 
         // one column j of the lane's rows; (MU, IU, DU) in = row r0-1, out = the lane's bottom row
         auto column = [&](const float (&aa)[RR], float &MU, float &IU, float &DU) {
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
             for (int k = 0; k < RR; ++k) {
                 const float MID = __fadd_rn(IU, DU);                   // :149-162
                 const float DDM = __fmul_rn(Mk[k], xi[k]);
-                const float IIMI = __fmul_rn(IU, c01);
+                const float IIMI = __fmul_rn(IU, k == 0 ? c01_0 : c01);
                 const float MIIDD = __fmul_rn(c09, MID);
                 const float Mn = __fmul_rn(aa[k], MM[k]);
                 const float In = __fmaf_rn(MU, de[k], IIMI);
@@ -203,10 +212,11 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
         // no activity test and no merge of state
         auto steady = [&](const float (&aa)[RR]) {
             float MU = rM, IU = rI, DU = rD;
-            if (lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }
+            if (!ABS && lg == 0) { MU = 0.f; IU = 0.f; DU = D0; }
             column(aa, MU, IU, DU);
             acc = __fadd_rn(acc, __fadd_rn(MU, IU));                       // kept by the bottom lane only
-            rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU);
+            if constexpr (ABS) { rM = shr_lane_fb(MU); rI = shr_lane_fb(IU); rD = shr_lane_fb(DU); }
+            else { rM = shr_lane_f(MU); rI = shr_lane_f(IU); rD = shr_lane_f(DU); }
         };
         {
             uint32_t hmin = valid ? H : 0u;

@@ -776,6 +776,13 @@ def test_pairhmm_edge_lengths(engine):
                               dq=rng.integers(10, 60, R)))
     args = _hmm_batch(pairs)
     np.testing.assert_allclose(engine.pairhmm_host(*args), O.pairhmm(*args), rtol=1e-5)
+    # every lane-group size with the longest read exactly filling the group's rows
+    # (boundary select) and one row short of it (the top lane's first row absorbs
+    # the boundary, pairhmm.hpp ABS)
+    for cap in (256, 255, 129, 128, 127, 64, 63, 33, 32, 31, 9, 8, 7):
+        sub = [p for p in pairs if len(p["read"]) <= cap]
+        a = _hmm_batch(sub)
+        np.testing.assert_allclose(engine.pairhmm_host(*a), O.pairhmm(*a), rtol=1e-5, err_msg=f"reads <= {cap}")
 
 
 def test_pairhmm_prior_table_vs_compare(engine):
