@@ -503,6 +503,9 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     uint64_t tb_words = (uint64_t)pad8(shape.max_q) * (pad8(shape.max_t) / 8);
     if (pl.packed16 && pl.tb)
         tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pad8(shape.max_q) * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
+#if GX_TB_STORE_MODE == 2
+    tb_words *= 2;   // timing probe: windows of G*R rows
+#endif
     int32_t *qend = out.q_end, *tend = out.t_end;
     const bool wf_start = pl.kind == PLAN_WAVEFRONT && (p.algo == 3 || p.algo == 2) && p.start_pos == 1 &&
                           (out.q_start || out.t_start);

@@ -82,6 +82,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #ifndef GX_WF16_TB_WAVES
 #define GX_WF16_TB_WAVES 2   // GLOBAL + traceback kernel
 #endif
+#ifndef GX_TB_STORE_MODE
+#define GX_TB_STORE_MODE 0   // GLOBAL+TB direction stores (1, 2: timing probes, see r02_tb_store_ab.md)
+#endif
 #ifndef GX_WF16_TB_ROWSYNC
 #define GX_WF16_TB_ROWSYNC 0
 #endif
@@ -674,9 +677,36 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 half_step(c + 3, 3, HB, HA);
 #endif
                 const uint32_t w = s >> 2;
+#if GX_TB_STORE_MODE == 1
+                // timing probe only: no direction stores (results invalid)
+                asm volatile("" ::"v"(dw[0]), "v"(dw[R - 1]));
+#else
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && w < W16[h]) {
+#if GX_TB_STORE_MODE == 2
+                        // timing probe only: lane-contiguous layout (walk not adapted)
+                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                                        (uint64_t)w * (G * R) + lg * 4;
+                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+                        for (int k = 0; k < R; k += 4)
+                            *reinterpret_cast<uint2 *>(dst + k * G) =
+                                make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
+                                           __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+#elif GX_TB_STORE_MODE == 3
+                        // non-temporal stores (the walk reads the flags once, later)
+                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                                        (uint64_t)w * xpad[h] + r0;
+                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+                        for (int k = 0; k < R; k += 4)
+                            if (r0 + k < xpad[h])
+                                __builtin_nontemporal_store(
+                                    (uint64_t)__builtin_amdgcn_perm(dw[k + 1], dw[k], sel) |
+                                        ((uint64_t)__builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel) << 32),
+                                    reinterpret_cast<uint64_t *>(dst + k));
+#else
                         uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
                                         (uint64_t)w * xpad[h] + r0;
                         const uint32_t sel = h ? 0x07060302u : 0x05040100u;
@@ -686,8 +716,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                 *reinterpret_cast<uint2 *>(dst + k) =
                                     make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
                                                __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+#endif
                     }
                 }
+#endif
             }
 #if GX_WF16_CAPTURE_TREE
 #pragma unroll
