@@ -498,14 +498,11 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     }
 
     // traceback storage: one word per (8-column strip, padded query row); the
-    // packed GLOBAL+TB kernel's skewed uint16 layout needs (t8 + G + 2) / 4 words
-    // of 16 bits per row instead (wavefront16.hpp)
+    // packed traceback kernels' skewed uint16 layout needs (t8 + G + 2) / 4 windows
+    // of G*R 16-bit entries instead (wavefront16.hpp)
     uint64_t tb_words = (uint64_t)pad8(shape.max_q) * (pad8(shape.max_t) / 8);
     if (pl.packed16 && pl.tb)
-        tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pad8(shape.max_q) * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
-#if GX_TB_STORE_MODE == 2
-    tb_words *= 2;   // timing probe: windows of G*R rows
-#endif
+        tb_words = std::max<uint64_t>(tb_words, (((uint64_t)pl.G16 * pl.R16 * ((pad8(shape.max_t) + pl.G16 + 2) / 4) / 2 + 3) & ~3ull));
     int32_t *qend = out.q_end, *tend = out.t_end;
     const bool wf_start = pl.kind == PLAN_WAVEFRONT && (p.algo == 3 || p.algo == 2) && p.start_pos == 1 &&
                           (out.q_start || out.t_start);
@@ -703,7 +700,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.a = p.match; T.b = p.mismatch; T.o = p.gap_open; T.e = p.gap_extend;
         T.is_local = p.algo == 3;
         T.pk_flags = nullptr;
-        T.pk_ppb = 1; T.pk_R = 1; T.pk_rmagic = 0;
+        T.pk_ppb = 1; T.pk_R = 1; T.pk_G = 1; T.pk_rmagic = 0;
         T.pk_fix = nullptr;
         T.slot_of = slot_of;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
@@ -723,6 +720,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             T.pk_flags = ws.misc.as<uint8_t>();
             T.pk_ppb = kWavesPerBlock * (64 / pl.G16) * 2;
             T.pk_R = pl.R16;
+            T.pk_G = pl.G16;
             T.pk_rmagic = (uint32_t)((0x100000000ull + pl.R16 - 1) / pl.R16);
             T.pk_fix = ws.aux.as<int32_t>();
         }

@@ -569,7 +569,7 @@ struct TbArgs {
     // pairs aligned by the packed GLOBAL+TB kernel (wavefront16.hpp) use its
     // skewed uint16 layout: flag per block of pk_ppb pairs, R rows per lane
     const uint8_t *pk_flags;
-    uint32_t pk_ppb, pk_R, pk_rmagic;   // pk_rmagic = ceil(2^32 / pk_R)
+    uint32_t pk_ppb, pk_R, pk_G, pk_rmagic;   // pk_rmagic = ceil(2^32 / pk_R)
     const int32_t *pk_fix;              // H' at the start cell (row ql, column tl) when both are pads
     const uint32_t *slot_of;            // pair -> slot of the DP launch when it ran sorted, or NULL
     int32_t sc_nn;                      // substitution score N vs N (GLOBAL rule)
@@ -617,7 +617,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     uint32_t prev = 0, opf = 0;
     int n_ops = 0, off = 0, count = 0, op_select = 3, op_shift = 0;
     // the walk reads one cell per step, mostly from consecutive rows: keep the
-    // 16-byte chunk it is in (4 rows of words / 8 rows of 16-bit flags) and the
+    // chunk it is in (16 bytes: 4 rows of words; 8 bytes: 4 rows of 16-bit flags) and the
     // current 8 codes of each sequence, so most steps make no memory access
     // (loaded once: the CIGAR byte stores may alias any input for the compiler)
     const uint32_t qoff = A.qoff[tid], toff = pk ? A.toff[tid] : 0u;
@@ -635,11 +635,18 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
         if (strip < tstrips) {
             if (pk) {
                 // wavefront16.hpp step_global_tb flags -> the reference's nibble
+                // window (column + lane) / 4 holds G*R entries, row lane*R + k at
+                // ((k/4)*G + lane)*4 + k%4 (wavefront16.hpp): 4 rows per 8-byte chunk
                 const uint32_t col = strip * 8 + c7;
-                const uint32_t s = col + __umulhi(row, A.pk_rmagic);   // column + lane of the row
-                const int64_t key = (int64_t)(s >> 2) * q8 + (row & ~7u);
-                if (key != chunk_key) { chunk = *reinterpret_cast<const uint4 *>(tb16 + key); chunk_key = key; }
-                const uint32_t fl = (pick4(chunk, (row & 7u) >> 1) >> (16 * (row & 1u) + (s & 3u))) & 0xFFFFu;
+                const uint32_t lane = __umulhi(row, A.pk_rmagic), k = row - lane * A.pk_R;
+                const uint32_t s = col + lane;
+                const int64_t key = (int64_t)(s >> 2) * (A.pk_G * A.pk_R) + ((k >> 2) * A.pk_G + lane) * 4;
+                if (key != chunk_key) {
+                    const uint2 c2 = *reinterpret_cast<const uint2 *>(tb16 + key);
+                    chunk = make_uint4(c2.x, c2.y, 0u, 0u);
+                    chunk_key = key;
+                }
+                const uint32_t fl = (((k & 2u) ? chunk.y : chunk.x) >> (16 * (k & 1u) + (s & 3u))) & 0xFFFFu;
                 const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
                 const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule

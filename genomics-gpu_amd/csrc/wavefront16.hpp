@@ -83,7 +83,7 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #define GX_WF16_TB_WAVES 2   // GLOBAL + traceback kernel
 #endif
 #ifndef GX_TB_STORE_MODE
-#define GX_TB_STORE_MODE 0   // GLOBAL+TB direction stores (1, 2: timing probes, see r02_tb_store_ab.md)
+#define GX_TB_STORE_MODE 0   // GLOBAL+TB direction stores (1: no-store timing probe, r02_tb_store_ab.md)
 #endif
 #ifndef GX_WF16_TB_ROWSYNC
 #define GX_WF16_TB_ROWSYNC 0
@@ -478,15 +478,15 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && w < W16[h]) {
+                        // lane-contiguous windows, as the GLOBAL+TB kernel's
                         uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                        (uint64_t)w * xpad[h] + r0;
+                                        (uint64_t)w * (G * R) + lg * 4;
                         const uint32_t sel = h ? 0x07060302u : 0x05040100u;
 #pragma unroll
                         for (int k = 0; k < R; k += 4)
-                            if (r0 + k < xpad[h])
-                                *reinterpret_cast<uint2 *>(dst + k) =
-                                    make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
-                                               __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+                            *reinterpret_cast<uint2 *>(dst + k * G) =
+                                make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
+                                           __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
                     }
                 }
             }
@@ -655,9 +655,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             recvF = (uint32_t)shr_lane((int32_t)f);
         };
         if constexpr (GTB) {
-            // Direction flags, skewed layout (read by tb_kernel): per pair, uint16
-            // [w][row] with w = (column + lane) / 4 holding the 4-step window's
-            // flags — every lane stores after the same steps, 4 rows per 8 bytes.
+            // Direction flags, skewed layout (read by tb_kernel): per pair, windows
+            // w = (column + lane) / 4 of G*R uint16 holding the 4-step window's flags,
+            // row lane*R + k at ((k/4)*G + lane)*4 + k%4 — every lane stores after the
+            // same steps, and the G lanes of a group write 8*G contiguous bytes per
+            // store (-5 % kernel time against [w][row], r02_tb_store_ab.md).
             static_assert(R % 4 == 0, "GLOBAL+TB packed shapes need R % 4 == 0");
             uint32_t W16[2];
 #pragma unroll
@@ -684,8 +686,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (valid[h] && w < W16[h]) {
-#if GX_TB_STORE_MODE == 2
-                        // timing probe only: lane-contiguous layout (walk not adapted)
+                        // window w of a pair: G*R uint16, row lg*R + k at ((k/4)*G + lg)*4 + k%4,
+                        // so a lane group's store is 8*G contiguous bytes
                         uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
                                         (uint64_t)w * (G * R) + lg * 4;
                         const uint32_t sel = h ? 0x07060302u : 0x05040100u;
@@ -694,29 +696,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                             *reinterpret_cast<uint2 *>(dst + k * G) =
                                 make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
                                            __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
-#elif GX_TB_STORE_MODE == 3
-                        // non-temporal stores (the walk reads the flags once, later)
-                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                        (uint64_t)w * xpad[h] + r0;
-                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
-#pragma unroll
-                        for (int k = 0; k < R; k += 4)
-                            if (r0 + k < xpad[h])
-                                __builtin_nontemporal_store(
-                                    (uint64_t)__builtin_amdgcn_perm(dw[k + 1], dw[k], sel) |
-                                        ((uint64_t)__builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel) << 32),
-                                    reinterpret_cast<uint64_t *>(dst + k));
-#else
-                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                        (uint64_t)w * xpad[h] + r0;
-                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
-#pragma unroll
-                        for (int k = 0; k < R; k += 4)
-                            if (r0 + k < xpad[h])
-                                *reinterpret_cast<uint2 *>(dst + k) =
-                                    make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
-                                               __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
-#endif
                     }
                 }
 #endif
