@@ -682,6 +682,33 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #if GX_TB_STORE_MODE == 1
                 // timing probe only: no direction stores (results invalid)
                 asm volatile("" ::"v"(dw[0]), "v"(dw[R - 1]));
+#elif GX_TB_STORE_MODE == 4
+                // every store of the window gets its own data registers, all formed
+                // before the first store: no VALU write waits for a store to read
+                // the register it would overwrite (the compiler otherwise reuses one
+                // pair for all of them)
+                {
+                    uint2 sv[2][R / 4];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+                        for (int k = 0; k < R; k += 4) {
+                            sv[h][k / 4] = make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
+                                                      __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+                            asm volatile("" : "+v"(sv[h][k / 4].x), "+v"(sv[h][k / 4].y));
+                        }
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if (valid[h] && w < W16[h]) {
+                            uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                                            (uint64_t)w * (G * R) + lg * 4;
+#pragma unroll
+                            for (int k = 0; k < R; k += 4) *reinterpret_cast<uint2 *>(dst + k * G) = sv[h][k / 4];
+                        }
+                    }
+                }
 #else
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
