@@ -731,23 +731,27 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
 }
 
 // ----------------------------------------------------------------------------
+#ifndef GX_HMM_RR
+#define GX_HMM_RR 8   // read rows per lane (A/B: 16)
+#endif
+constexpr int kHmmRows = GX_HMM_RR;
 using HmmFn = void (*)(HmmArgs);
 template <bool QUALS, bool ABS>
 static HmmFn hmm_lookup(int G) {
     switch (G) {
-        case 4: return &pairhmm_kernel<4, 8, QUALS, ABS>;
-        case 8: return &pairhmm_kernel<8, 8, QUALS, ABS>;
-        case 16: return &pairhmm_kernel<16, 8, QUALS, ABS>;
-        case 32: return &pairhmm_kernel<32, 8, QUALS, ABS>;
-        case 64: return &pairhmm_kernel<64, 8, QUALS, ABS>;
+        case 4: return &pairhmm_kernel<4, kHmmRows, QUALS, ABS>;
+        case 8: return &pairhmm_kernel<8, kHmmRows, QUALS, ABS>;
+        case 16: return &pairhmm_kernel<16, kHmmRows, QUALS, ABS>;
+        case 32: return &pairhmm_kernel<32, kHmmRows, QUALS, ABS>;
+        case 64: return &pairhmm_kernel<64, kHmmRows, QUALS, ABS>;
         default: return nullptr;
     }
 }
 
-// lanes per pair for a read of max_r rows: 8 rows per lane, G in {4, ..., 64}
+// lanes per pair for a read of max_r rows: kHmmRows (8) rows per lane, G in {4, ..., 64}
 int pairhmm_group(uint32_t max_r) {
     for (int g : {4, 8, 16, 32, 64})
-        if ((uint32_t)g * 8 >= max_r) return g;
+        if ((uint32_t)g * kHmmRows >= max_r) return g;
     return 0;
 }
 
@@ -762,12 +766,12 @@ static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0,
     A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
     // reads shorter than the group's rows: the top lane's first row is virtual and
     // absorbs the boundary (pairhmm.hpp ABS)
-    const bool absorb = (uint32_t)G * 8 > max_r;
+    const bool absorb = (uint32_t)G * kHmmRows > max_r;
     HmmFn fn = quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
                      : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G));
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
-    // 8 rows x 64 lanes x 4 bytes
-    const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * 8 * 64 * 4;
+    // kHmmRows rows x 64 lanes x 4 bytes
+    const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * kHmmRows * 64 * 4;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
     if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);
