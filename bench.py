@@ -107,6 +107,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave out the all-gather of scores")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo stages the exchange "
+                         "through host memory, so several ranks can share one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's shard of the global batch as a JSON line and exit (no GPU call)")
     return ap.parse_args()
@@ -491,16 +494,38 @@ def main():
         return
 
     import torch.distributed as dist
-    dev = torch.device("cuda", local_rank)
+    # ranks beyond the visible devices share them (LOCAL_RANK % device_count): with the
+    # gloo backend, the exact N-rank path (spawn -> engine -> exchange -> parity) runs on
+    # a box with fewer GPUs than ranks; RCCL needs one rank per device
+    n_dev = torch.cuda.device_count()
+    dev_index = local_rank % max(n_dev, 1)
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
+    backend = args.dist_backend
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        if backend == "nccl" and world > n_dev:
+            sys.exit(f"bench.py: {world} ranks over {n_dev} GPUs needs --dist-backend gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=dev)
+        else:
+            dist.init_process_group("gloo", init_method="env://")
 
-    eng = G.Engine(local_rank)
+    def allreduce(t, op):
+        """all_reduce of a small device tensor (through host memory under gloo)."""
+        if world == 1:
+            return t
+        if backend == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            return h.to(t.device)
+        dist.all_reduce(t, op=op)
+        return t
+
+    eng = G.Engine(dev_index)
     stream = torch.cuda.Stream(dev)      # a real (non-null) stream: kernels and timing events share it
     torch.cuda.set_stream(stream)
-    gather = D.ScoreGather(counts, world, dev, dtype=torch.float32 if kind == 5 else torch.int32) \
-        if do_gather else None
+    gather = D.ScoreGather(counts, world, dev, dtype=torch.float32 if kind == 5 else torch.int32,
+                           backend=backend) if do_gather else None
     t_syn = time.perf_counter()
     if kind == 6:
         nv = synth_nvbio(start, n, seed)
@@ -605,7 +630,7 @@ def main():
     gath_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     t = torch.tensor([elapsed, kern_ms, gath_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = allreduce(t, dist.ReduceOp.MAX)
     elapsed, kern_ms, gath_ms = (float(x) for x in t)
 
     # ---- parity: this rank's shard against the oracle (the CPU baseline at N = 1) ----
@@ -643,7 +668,7 @@ def main():
         gather_bad = 0
         if gather is not None:
             # the gathered scores (timed steps' exchange) against every rank's oracle scores
-            og = D.ScoreGather(counts, world, dev, dtype=gather.buf.dtype)
+            og = D.ScoreGather(counts, world, dev, dtype=gather.buf.dtype, backend=backend)
             og.buf[:m] = torch.as_tensor(np.asarray(ref_scores), device=dev)
             og()
             gfull = gather.out.cpu().numpy()
@@ -657,7 +682,7 @@ def main():
                 else:
                     gather_bad += int(np.count_nonzero(a != b))
         if world > 1:
-            dist.all_reduce(tot)
+            tot = allreduce(tot, dist.ReduceOp.SUM)
         parity = {"pairs_checked": int(tot[0]), "mismatches": int(tot[1]),
                   "by_field_rank0": mism, **extra,
                   "tolerance": "rtol 1e-5" if kind == 5 else "bit-exact",
@@ -745,7 +770,10 @@ def main():
             "config": {"workload": wl["label"], "pairs_global": n_global, "pairs_rank0": n,
                        "cells_rank0_step": cells_per_step, "plan": plan,
                        "parallelism": f"dp{world} (cell-balanced contiguous shards of one global batch)" +
-                                      (", RCCL all-gather of scores in every step" if gather else ""),
+                                      ((", RCCL all-gather of scores in every step" if backend == "nccl" else
+                                        ", gloo all-gather of scores (through host memory) in every step")
+                                       if gather else ""),
+                       **({"dist_backend": backend, "devices": n_dev} if world > 1 else {}),
                        "synth_s_rank0": round(synth_s, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,

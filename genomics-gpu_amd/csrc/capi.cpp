@@ -57,6 +57,8 @@ struct gasalx_engine {
         }                                                                            \
     } while (0)
 
+hipStream_t gx::engine_stream(gasalx_engine *e) { return e->stream; }
+
 namespace {
 
 __attribute__((unused)) uint32_t host_max(const uint32_t *a, uint32_t n) {
@@ -295,6 +297,7 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         shape.max_q = mq;
         shape.max_t = mt;
         shape.sort = gx::uneven_lengths(*params, hb->q_lens + i0, hb->t_lens + i0, m);
+        shape.tb_split = false;   // the two slots' streams already overlap one chunk's walk with the next DP
         if ((rc = gx::align_device(s.ws, *params, db, dout, s.st, shape))) {
             for (HostSlot &x : eng->slot) (void)hipStreamSynchronize(x.st);
             return rc;

@@ -37,6 +37,11 @@ void DevBuf::release() {
     bytes = 0;
 }
 void Workspace::release_all() {
+    if (walk_stream) { (void)hipStreamSynchronize(walk_stream); (void)hipStreamDestroy(walk_stream); walk_stream = nullptr; }
+    for (Workspace *w : sides) { w->release_all(); delete w; }
+    sides.clear();
+    for (hipEvent_t *x : {&fork, &join, &dp_done})
+        if (*x) { (void)hipEventDestroy(*x); *x = nullptr; }
     for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
                       &rev_t, &rev_meta, &sort_meta}) b->release();
 }
@@ -200,7 +205,9 @@ static bool local16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
     const int64_t k = local16_k(p), sn = local16_sn(p);
     if (p.match + k > 255 || k - p.mismatch > 255 || sn + k > 255) return false;
     if (q8 > 65535 || t8 / 8 > 65535) return false;   // rows and strips are tracked in 16 bits
-    const int64_t hmax = (int64_t)std::max<int64_t>(p.match, sn) * std::min(q8, t8);
+    // largest gain of one cell: match, a negative mismatch or a negative N penalty
+    const int64_t step = std::max<int64_t>({(int64_t)p.match, -(int64_t)p.mismatch, sn});
+    const int64_t hmax = step * std::min(q8, t8);
     return hmax + local16_base(p) <= 0x7BFF && hmax * 8 + 7 + 0x400 <= 0x7BFF;
 }
 
@@ -446,6 +453,27 @@ static int geometry_perm(Workspace &ws, const gasalx_batch &b, const BatchShape 
     return GASALX_OK;
 }
 
+// Everything after align_device's prologue, over the pairs of b (a whole batch or one
+// chunk of it).  walk_qseq: the query codes the traceback walk reads when the CIGAR
+// buffer overlays the query batch (copied once by the prologue), else NULL.
+enum { PHASE_DP = 1, PHASE_WALK = 2, PHASE_ALL = 3 };
+static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, const gasalx_batch &b,
+                      const gasalx_results &out, hipStream_t st, const BatchShape &shape, uint64_t cigar_cap,
+                      const uint8_t *walk_qseq, int phases = PHASE_ALL);
+
+// GASALX_TB_CHUNKS: chunks of a traceback batch (A/B runs; 1 = one launch pair)
+static uint32_t tb_chunks(uint32_t n) {
+    static const int force = [] {
+        const char *e = std::getenv("GASALX_TB_CHUNKS");
+        return e ? std::atoi(e) : 0;
+    }();
+    (void)n;
+    // default one launch pair: the walk is latency-bound (a 25 K-pair chunk's walk takes
+    // 0.51 ms, the whole 100 K-pair batch's 0.70 ms, profiles/r03_tb_chunks.md), so the
+    // last chunk's walk costs nearly the whole walk again and chunking only adds DP tails
+    return force > 0 ? (uint32_t)force : 1u;
+}
+
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
                  hipStream_t st, const BatchShape &shape, uint64_t cigar_cap) {
     if (b.n_alns == 0 || b.q_bytes == 0 || b.t_bytes == 0) { set_error("empty batch"); return GASALX_EINVAL; }
@@ -470,9 +498,79 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         HIPCHK(hipMemcpyAsync(out.n_cigar_ops, b.q_lens, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     if (pl.kind == PLAN_NONE) return GASALX_OK;   // UNKNOWN / MICROLOCAL: nothing launched
 
+    // the walk writes CIGARs over the unpacked query batch when that is the cigar
+    // buffer (get_tb.h:94) but the packed kernels' walk reads query codes from it:
+    // give it a copy, taken before any walk runs
+    const uint8_t *walk_qseq = nullptr;
+    if (runs_tb && out.cigar && out.n_cigar_ops && pl.kind == PLAN_WAVEFRONT && pl.packed16 && !pl.need_pack) {
+        const uint8_t *c0 = out.cigar, *q0 = b.q_batch;
+        const uint64_t cap = cigar_cap ? cigar_cap : b.q_bytes;
+        if (c0 < q0 + b.q_bytes && q0 < c0 + cap) {
+            HIPCHK(ws.packed_q.reserve(b.q_bytes));
+            HIPCHK(hipMemcpyAsync(ws.packed_q.p, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
+            walk_qseq = ws.packed_q.as<uint8_t>();
+        }
+    }
+
+    // Traceback in chunks (GASALX_TB_CHUNKS > 1): the DP kernel is VALU-bound, the
+    // walk (tb_kernel) bound by the latency of its dependent loads.  Chunk k's DP runs
+    // on the caller's stream, its walk on a second stream after an event, beside the
+    // following DPs.  Every chunk has its own workspace (direction data, flags, ends).
+    const uint32_t chunks = runs_tb && out.cigar && out.n_cigar_ops && shape.tb_split && pl.kind == PLAN_WAVEFRONT &&
+                                    !pl.need_pack ? tb_chunks(n) : 1;
+    if (chunks > 1) {
+        while (ws.sides.size() + 1 < chunks) ws.sides.push_back(new Workspace());
+        for (Workspace *w : ws.sides) w->device = ws.device;
+        if (!ws.walk_stream) HIPCHK(hipStreamCreateWithFlags(&ws.walk_stream, hipStreamNonBlocking));
+        for (hipEvent_t *x : {&ws.fork, &ws.join, &ws.dp_done})
+            if (!*x) HIPCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(ws.fork, st));
+        HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.fork, 0));
+        const uint32_t per = (n + chunks - 1) / chunks;
+        int rc = GASALX_OK;
+        for (uint32_t c = 0, i0 = 0; i0 < n && rc == GASALX_OK; c++, i0 += per) {
+            const uint32_t m = std::min(per, n - i0);
+            gasalx_batch cb = b;
+            cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
+            if (cb.q_ops) cb.q_ops += i0;
+            if (cb.t_ops) cb.t_ops += i0;
+            if (cb.seed_scores) cb.seed_scores += i0;
+            cb.n_alns = m;
+            gasalx_results co = out;
+            for (int32_t **f : {&co.aln_score, &co.q_end, &co.t_end, &co.q_start, &co.t_start, &co.aln_score2,
+                                &co.q_end2, &co.t_end2})
+                if (*f) *f += i0;
+            co.n_cigar_ops += i0;      // the CIGAR buffer is addressed by query offsets
+            BatchShape cs = sized;
+            cs.n = m;
+            const Plan cp = make_plan(p, cs, has_ops);
+            Workspace &w = c ? *ws.sides[c - 1] : ws;
+            rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_DP);
+            if (rc) break;
+            HIPCHK(hipEventRecord(ws.dp_done, st));
+            HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.dp_done, 0));
+            rc = align_body(w, p, cp, cb, co, ws.walk_stream, cs, cigar_cap, walk_qseq, PHASE_WALK);
+        }
+        // join: the caller's stream continues after the walks
+        HIPCHK(hipEventRecord(ws.join, ws.walk_stream));
+        HIPCHK(hipStreamWaitEvent(st, ws.join, 0));
+        return rc;
+    }
+    return align_body(ws, p, pl, b, out, st, sized, cigar_cap, walk_qseq);
+}
+
+static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, const gasalx_batch &b,
+                      const gasalx_results &out, hipStream_t st, const BatchShape &shape, uint64_t cigar_cap,
+                      const uint8_t *walk_qseq, int phases) {
+    const bool dp = phases & PHASE_DP;   // a walk-only call (chunked traceback) recomputes pointers, launches the walk
+    const bool has_ops = b.q_ops && b.t_ops;
+    const uint32_t n = b.n_alns;
+    const bool tb = p.start_pos == 2;
+    const bool runs_tb = tb && (p.algo == 1 || p.algo == 3) && pl.kind != PLAN_NONE;
+
     const uint8_t *qsrc = b.q_batch, *tsrc = b.t_batch;
     int packed = p.is_packed ? 1 : 0;
-    if (pl.need_pack) {
+    if (pl.need_pack) {   // (never in a walk-only call: chunked traceback excludes need_pack)
         const uint32_t qw = b.q_bytes / 8, tw = b.t_bytes / 8;
         HIPCHK(ws.packed_q.reserve((size_t)qw * 4 + 16));
         HIPCHK(ws.packed_t.reserve((size_t)tw * 4 + 16));
@@ -539,19 +637,21 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             if (2 * sh <= 64 * 1024) {
                 HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + (size_t)(s8w + 1) * 8 + 64));
                 uint32_t *perm = ws.sort_meta.as<uint32_t>(), *inv = perm + n, *hist = inv + n, *cursor = hist + s8w + 1;
-                HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-                rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
-                rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
-                rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, cursor,
-                                                                          perm, inv);
-                HIPCHK(hipGetLastError());
+                if (dp) {
+                    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+                    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
+                    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
+                    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w,
+                                                                              cursor, perm, inv);
+                    HIPCHK(hipGetLastError());
+                }
                 A.perm = perm;
                 slot_of = inv;
             }
         }
-        int rc = launch_wavefront(ws, pl, p, A, st);
+        int rc = dp ? launch_wavefront(ws, pl, p, A, st) : GASALX_OK;
         if (rc) return rc;
-        if (wf_start) {
+        if (wf_start && dp) {
             if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {
                 set_error("WITH_START: batch too large for one call (reversed slots exceed 4 GB)");
                 return GASALX_ERANGE;
@@ -560,7 +660,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
                                qend, tend, out.q_start, out.t_start, st);
             if (rc) return rc;
         }
-    } else {
+    } else if (dp) {
         GenArgs A;
         std::memset(&A, 0, sizeof(A));
         A.qw = ws.packed_q.as<uint32_t>(); A.tw = ws.packed_t.as<uint32_t>();
@@ -689,7 +789,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         HIPCHK(hipGetLastError());
     }
 
-    if (runs_tb && out.cigar && out.n_cigar_ops) {
+    if (runs_tb && out.cigar && out.n_cigar_ops && (phases & PHASE_WALK)) {
         TbArgs T;
         T.tb = ws.tb.as<uint32_t>(); T.tb_pair_words = tb_words;
         T.qlen = b.q_lens; T.tlen = b.t_lens; T.qoff = b.q_offsets;
@@ -705,16 +805,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         T.slot_of = slot_of;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
         T.qseq = qsrc; T.tseq = tsrc; T.toff = b.t_offsets; T.seq_packed = packed;
-        if (pl.kind == PLAN_WAVEFRONT && pl.packed16 && !pl.need_pack) {
-            // the walk writes CIGARs over the unpacked query batch when that is the
-            // cigar buffer (get_tb.h:94) but reads query codes: give it a copy
-            const uint8_t *c0 = out.cigar, *q0 = b.q_batch;
-            if (c0 < q0 + b.q_bytes && q0 < c0 + T.cigar_cap) {
-                HIPCHK(ws.packed_q.reserve(b.q_bytes));
-                HIPCHK(hipMemcpyAsync(ws.packed_q.p, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
-                T.qseq = ws.packed_q.as<uint8_t>();
-            }
-        }
+        if (walk_qseq) T.qseq = walk_qseq;   // align_device's copy of the query codes
         T.nval = p.n_code & 0xF; T.has_npen = p.has_n_penalty; T.npen = p.n_penalty;
         if (pl.kind == PLAN_WAVEFRONT && pl.packed16) {
             T.pk_flags = ws.misc.as<uint8_t>();

@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "gasalx.h"
 
@@ -33,6 +34,12 @@ struct Workspace {
     DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
     DevBuf rev_q, rev_t, rev_meta;  // WITH_START: reversed slots, their offsets/lengths, reverse results
     DevBuf sort_meta;               // length sort of the forward pass: perm, inverse, histogram
+    // traceback batches in chunks (align_device, GASALX_TB_CHUNKS): DPs on the
+    // caller's stream, walks on walk_stream; one workspace per further chunk; all
+    // created on first use
+    hipStream_t walk_stream = nullptr;
+    std::vector<Workspace *> sides;
+    hipEvent_t fork = nullptr, join = nullptr, dp_done = nullptr;
     void release_all();
 };
 
@@ -62,6 +69,7 @@ struct BatchShape {
     uint32_t max_q = 0, max_t = 0;
     bool sort = false;   // lengths are uneven: run the wavefront kernels over pairs sorted by step-axis length
     uint32_t n = 0;      // pairs in the launch (0 = unknown: shapes for large batches)
+    bool tb_split = true; // traceback: chunks on two streams so a chunk's walk overlaps the next DP
 };
 
 Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
@@ -105,6 +113,9 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
                     hipStream_t stream);
 std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text,
                          uint32_t text_bits);
+
+// The engine's own stream (capi.cpp; gasalx_engine is opaque elsewhere).
+hipStream_t engine_stream(gasalx_engine *e);
 
 void set_error(const std::string &msg);
 const char *last_error();

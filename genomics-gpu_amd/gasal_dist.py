@@ -27,17 +27,19 @@ def cell_counts(q_lens, t_lens) -> np.ndarray:
 def shard_bounds(cells: np.ndarray, world: int) -> list[tuple[int, int]]:
     """Contiguous [start, end) ranges, one per rank, balancing Σ cells.
 
-    Boundary k is the first pair whose inclusive prefix sum reaches k/world of
-    the total, so every range holds at most one pair's cells above its share."""
+    Boundary k is one past the first pair whose inclusive prefix sum reaches k/world
+    of the total (csum·world >= total·k, in integers), so every range holds at most
+    one pair's cells above its share.  The library's gasalx_shard_bounds (the
+    multi-GPU C-ABI, csrc/multi.cpp) applies the same rule."""
     if world < 1:
         raise ValueError("world must be >= 1")
     n = len(cells)
     csum = np.cumsum(np.asarray(cells, np.int64))
     total = int(csum[-1]) if n else 0
+    scaled = [int(c) * world for c in csum] if n and total * world >= 2 ** 62 else csum * world
     cuts = [0]
     for k in range(1, world):
-        target = total * k / world
-        cuts.append(int(np.searchsorted(csum, target, side="left")) + (1 if n else 0))
+        cuts.append(int(np.searchsorted(scaled, total * k, side="left")) + (1 if n else 0))
     cuts.append(n)
     cuts = [min(max(c, 0), n) for c in cuts]
     for k in range(1, len(cuts)):          # monotone (empty ranges allowed)
@@ -75,7 +77,7 @@ class ScoreGather:
     tensor on every rank.  `buf` is the rank's padded result tensor; the aligner
     writes its first n_local entries in place."""
 
-    def __init__(self, counts: list[int], world: int, device, dtype=None):
+    def __init__(self, counts: list[int], world: int, device, dtype=None, backend: str = "nccl"):
         import torch
         self.counts = list(counts)
         self.world = world
@@ -84,9 +86,20 @@ class ScoreGather:
         self.buf = torch.zeros(self.cap, dtype=dt, device=device)
         self.out = torch.zeros((world, self.cap), dtype=dt, device=device)
         self._parts = list(self.out.unbind(0))
+        # gloo with device tensors: stage through host memory (ranks may share a GPU)
+        self._host = backend == "gloo" and self.buf.device.type != "cpu"
+        if self._host:
+            self._hbuf = torch.zeros(self.cap, dtype=dt)
+            self._hout = torch.zeros((world, self.cap), dtype=dt)
+            self._hparts = list(self._hout.unbind(0))
 
     def __call__(self):
         import torch.distributed as dist
+        if self._host:
+            self._hbuf.copy_(self.buf)
+            dist.all_gather(self._hparts, self._hbuf)
+            self.out.copy_(self._hout)
+            return
         dist.all_gather(self._parts, self.buf)
 
     def full(self) -> np.ndarray:

@@ -33,7 +33,11 @@ EXPORTS = (
     "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
     "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
     "gasalx_nv_score_device", "gasalx_nv_score_host", "gasalx_nv_describe_plan",
+    "gasalx_multi_create", "gasalx_multi_destroy", "gasalx_multi_info", "gasalx_multi_engine",
+    "gasalx_shard_bounds", "gasalx_multi_align_host", "gasalx_multi_pairhmm_host",
+    "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather",
 )
+MULTI_RCCL = 1
 
 # nvbio front-end (gasalx_nv_*): aligners and AlignmentType (nvbio/alignment/alignment_base.h:54)
 NV_ED, NV_SW, NV_GOTOH = 0, 1, 2
@@ -102,6 +106,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libgasal not built: {LIB_PATH} (run __graft_entry__.build())")
+        # torch (when present) first: its bundled HIP runtime (soname libamdhip64.so.7)
+        # must be the one libgasal binds to; loading libgasal first brings in /opt/rocm's
+        # copy, and two HIP runtimes in one process do not share the device (torch then
+        # reports no GPU).  INTEGRATION.md, "One HIP runtime per process".
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _lib = ctypes.CDLL(LIB_PATH)
         _lib.gasalx_last_error.restype = ctypes.c_char_p
         for name in EXPORTS:
@@ -215,9 +227,19 @@ OUT_FIELDS = ("score", "q_end", "t_end", "q_start", "t_start", "score2", "q_end2
 
 
 class _PinnedArray(np.ndarray):
-    """ndarray over page-locked bytes; holds its PinnedHost so the memory lives as
-    long as any view of it does."""
+    """ndarray over page-locked bytes; holds the allocation's owner so the memory
+    lives as long as any view of it does."""
     _owner = None
+
+
+class _PinnedOwner:
+    """The allocation itself: freed (gasalx_host_free) as soon as the last array
+    referring to it is gone.  Nothing refers back to the arrays, so no reference
+    cycle waits for the cyclic collector."""
+
+    def __init__(self, ptr: int):
+        self.ptr = ptr
+        self._finalizer = weakref.finalize(self, lib().gasalx_host_free, ctypes.c_void_p(ptr))
 
 
 class PinnedHost:
@@ -225,19 +247,19 @@ class PinnedHost:
     caller-owned buffers such as align_host(cigar_out=...), as the reference's host_res
     is pinned (res.cpp:8-70).
 
-    `array` (and every view or slice of it) keeps this object alive, and the memory
-    is freed only when the last of them is gone: close() drops this handle's own
-    reference, it never frees memory an array still points at."""
+    `array` (and every view or slice of it) keeps the allocation alive, and the memory
+    is freed as soon as the last of them is gone (this handle included): close()
+    drops this handle's own reference, it never frees memory an array still points at."""
 
     def __init__(self, nbytes: int):
         L = lib()
         self._p = ctypes.c_void_p()
         _check(L.gasalx_host_alloc(ctypes.c_uint64(max(int(nbytes), 1)), ctypes.byref(self._p)), "host_alloc")
         self.nbytes = int(nbytes)
-        self._finalizer = weakref.finalize(self, L.gasalx_host_free, ctypes.c_void_p(self._p.value))
+        owner = _PinnedOwner(self._p.value)
         raw = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self._p.value))
         arr = raw[:self.nbytes].view(_PinnedArray)
-        arr._owner = self
+        arr._owner = owner
         self.array = arr
 
     def close(self):
@@ -355,6 +377,89 @@ class Engine:
                        g("haps"), g("hap_offsets"), g("hap_lens"), read_bytes, hap_bytes, n, max_r, max_h)
         _check(lib().gasalx_pairhmm_device(self._h, ctypes.byref(hb), ctypes.c_void_p(result_ptr),
                                            ctypes.c_void_p(stream or None)), "pairhmm_device")
+
+
+def shard_bounds(a, b, world: int) -> list:
+    """gasalx_shard_bounds: contiguous [start, end) ranges balancing sum(a[i] * b[i])."""
+    a = np.ascontiguousarray(a, np.uint32)
+    b = np.ascontiguousarray(b, np.uint32)
+    out = np.zeros(world + 1, np.uint32)
+    _check(lib().gasalx_shard_bounds(_p(a), _p(b), ctypes.c_uint32(len(a)), world, _p(out)), "shard_bounds")
+    return [(int(out[k]), int(out[k + 1])) for k in range(world)]
+
+
+class Multi:
+    """A multi-GPU group (gasalx_multi): one engine per device entry, host batches split
+    into cell-balanced contiguous shards with one host thread per entry."""
+
+    def __init__(self, devices, rccl: bool = False):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        self.devices = list(devices)
+        self._h = ctypes.c_void_p()
+        _check(lib().gasalx_multi_create(devs, len(devices), MULTI_RCCL if rccl else 0, ctypes.byref(self._h)),
+               "multi_create")
+
+    def close(self):
+        if self._h:
+            lib().gasalx_multi_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def uses_rccl(self) -> bool:
+        n, r = ctypes.c_int(), ctypes.c_int()
+        _check(lib().gasalx_multi_info(self._h, ctypes.byref(n), ctypes.byref(r)), "multi_info")
+        return bool(r.value)
+
+    def align_host(self, batch: "Batch", params: "Params", q_ops=None, t_ops=None, seed_scores=None, fields=None):
+        n = batch.n
+        out = {k: np.full(n, SENTINEL, np.int32) for k in (OUT_FIELDS if fields is None else fields)}
+        tb = params.start_pos == WITH_TB
+        cigar = np.zeros(batch.q_bytes if tb else 0, np.uint8)
+        n_ops = np.zeros(n if tb else 0, np.uint32)
+        qo = None if q_ops is None else np.ascontiguousarray(q_ops, np.uint8)
+        to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
+        sd = None if seed_scores is None else np.ascontiguousarray(seed_scores, np.uint32)
+        cb = CBatch(_p(batch.q_data), _p(batch.q_offsets), _p(batch.q_lens), _p(batch.t_data), _p(batch.t_offsets),
+                    _p(batch.t_lens), batch.q_bytes, batch.t_bytes, n, _p(qo), _p(to), _p(sd), 0, 0)
+        cr = CResults(*(_p(out[k]) if k in out else None for k in OUT_FIELDS), _p(cigar) if tb else None,
+                      _p(n_ops) if tb else None)
+        _check(lib().gasalx_multi_align_host(self._h, ctypes.byref(params), ctypes.byref(cb), ctypes.byref(cr)),
+               "multi_align_host")
+        out["cigar"] = cigar
+        out["n_ops"] = n_ops
+        return out
+
+    def pairhmm_host(self, reads, read_off, read_len, qm, delta, xiksi, alpha, haps, hap_off, hap_len):
+        c = lambda a, t: np.ascontiguousarray(a, t)
+        reads, haps = c(reads, np.uint8), c(haps, np.uint8)
+        arrs = [c(read_off, np.uint32), c(read_len, np.uint32), c(qm, np.float32), c(delta, np.float32),
+                c(xiksi, np.float32), c(alpha, np.float32), c(hap_off, np.uint32), c(hap_len, np.uint32)]
+        n = len(arrs[1])
+        res = np.zeros(n, np.float32)
+        hb = CHmmBatch(_p(reads), _p(arrs[0]), _p(arrs[1]), _p(arrs[2]), _p(arrs[3]), _p(arrs[4]), _p(arrs[5]),
+                       _p(haps), _p(arrs[6]), _p(arrs[7]), len(reads), len(haps), n, 0, 0)
+        _check(lib().gasalx_multi_pairhmm_host(self._h, ctypes.byref(hb), _p(res)), "multi_pairhmm_host")
+        return res
+
+    def pairhmm_quals_host(self, hmm: "HmmData"):
+        res = np.zeros(hmm.n, np.float32)
+        hb = hmm.cstruct()
+        _check(lib().gasalx_multi_pairhmm_quals_host(self._h, ctypes.byref(hb), _p(res)), "multi_pairhmm_quals_host")
+        return res
+
+    def allgather_ptrs(self, send_ptrs, recv_ptrs, nbytes: int, streams=None):
+        """Device buffers (integer addresses), one send and one recv per entry."""
+        k = len(self.devices)
+        snd = (ctypes.c_void_p * k)(*send_ptrs)
+        rcv = (ctypes.c_void_p * k)(*recv_ptrs)
+        sts = None if streams is None else (ctypes.c_void_p * k)(*streams)
+        _check(lib().gasalx_multi_allgather(self._h, snd, rcv, ctypes.c_uint64(nbytes), sts), "multi_allgather")
 
 
 def synth_spec(kind: int):

@@ -257,6 +257,40 @@ int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, u
                          const gasalx_nv_strings *patterns, uint64_t pattern_words, const gasalx_nv_strings *texts,
                          uint64_t text_words, int32_t *scores, int16_t *scores16);
 
+/* Multi-GPU from one host process.  A group holds one engine per
+ * entry of a device list (entries may repeat a device); a host batch is split into
+ * contiguous ranges of pairs with equal cell counts (Σ ql·tl; gasalx_shard_bounds),
+ * and one host thread per entry runs gasalx_align_host (or the PairHMM call) on its
+ * range, writing into that range of the caller's result arrays.  The reference's
+ * pattern is STAR's static split (Non-CDP/STAR/src/cuda-nw.cu:296-367: per-GPU
+ * workload, cudaSetDevice, one stream per device, disjoint host result ranges);
+ * GASAL2 itself exposes only gasal_set_device (interfaces.cpp:98-125).
+ * GASALX_MULTI_RCCL: build an RCCL communicator over the list (ncclCommInitAll, when
+ * the entries are distinct devices and librccl can be opened) for
+ * gasalx_multi_allgather; otherwise that call uses peer copies. */
+typedef struct gasalx_multi gasalx_multi;
+enum { GASALX_MULTI_RCCL = 1 };
+
+int gasalx_multi_create(const int *devices, int n_devices, uint32_t flags, gasalx_multi **out);
+int gasalx_multi_destroy(gasalx_multi *m);
+int gasalx_multi_info(const gasalx_multi *m, int *n_devices, int *uses_rccl);
+/* The engine of entry `index` (owned by the group), e.g. for device-resident calls. */
+int gasalx_multi_engine(gasalx_multi *m, int index, gasalx_engine **out);
+/* Contiguous ranges [bounds[k], bounds[k+1]) (world + 1 entries) balancing Σ a[i]·b[i]:
+ * boundary k is one past the first pair whose prefix sum reaches k/world of the total. */
+int gasalx_shard_bounds(const uint32_t *a, const uint32_t *b, uint32_t n, int world, uint32_t *bounds);
+/* Host arrays in and out, as gasalx_align_host.  WITH_TB: the shards' query byte ranges
+ * must not overlap (each pair's CIGAR lands at its query offset, get_tb.h:94). */
+int gasalx_multi_align_host(gasalx_multi *m, const gasalx_params *params, const gasalx_batch *host_batch,
+                            const gasalx_results *host_out);
+int gasalx_multi_pairhmm_host(gasalx_multi *m, const gasalx_hmm_batch *host_batch, float *host_result);
+int gasalx_multi_pairhmm_quals_host(gasalx_multi *m, const gasalx_hmm_qual_batch *host_batch, float *host_result);
+/* The exchange step: entry i's `bytes` at send[i] (device memory of its device) land at
+ * recv[j] + i * bytes on every entry j.  streams: one hipStream_t per entry (the call
+ * is then asynchronous), or NULL for the engines' streams and a synchronous call. */
+int gasalx_multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
+                           void *const *streams);
+
 /* Synthetic workloads of SURVEY.md §8(d) (benchmark/test data, std::mt19937_64).
  * Writes a GASAL2-layout batch (N_CODE padding) into caller buffers sized by
  * gasalx_synth_sizes.  kind: 1..4 = configs 1..4.  Pairs come in blocks of 65,536,

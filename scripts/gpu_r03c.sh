@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 3: traceback walk with the 2x2 chunk block cache: parity + config 3 / LOCAL+TB.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r03c
+mkdir -p $O
+fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "traceback or config3 or tb or gainful or ksw or local16" > $O/tb.txt 2>&1
+rc=$?; echo "tb rc=$rc"; tail -3 $O/tb.txt; if fatal $rc; then exit $rc; fi
+for c in 1 2; do
+  GASALX_TB_CHUNKS=$c timeout -k 10 300 python -u bench.py --workload nw_tb --steps 10 --warmup 2 --no-cpu --no-e2e --parity-pairs 100000 > $O/nw_tb_c$c.json 2> $O/nw_tb_c$c.err
+  rc=$?; echo "nw_tb chunks=$c rc=$rc $(python -c "import json;d=json.load(open('$O/nw_tb_c$c.json'));print(d['value'],d['parity']['mismatches'])" 2>/dev/null)"
+  if fatal $rc; then exit $rc; fi
+done
+timeout -k 10 300 python -u bench.py --workload sw_local_tb --steps 5 --warmup 1 --no-cpu --no-e2e --parity-pairs 200000 > $O/swtb.json 2> $O/swtb.err
+rc=$?; echo "sw_local_tb rc=$rc $(python -c "import json;d=json.load(open('$O/swtb.json'));print(d['value'],d['parity']['mismatches'])" 2>/dev/null)"
+if fatal $rc; then exit $rc; fi
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_nw -o run -- python3 $GRAFT_REPO_ROOT/bench.py --workload nw_tb --steps 10 --warmup 2 --no-cpu --no-e2e --parity-pairs 0 > $GRAFT_REPO_ROOT/$O/prof_nw.json 2>&1
+echo "prof rc=$?"
+exit 0

@@ -101,3 +101,16 @@ def test_gloo_bench_shard_path(tmp_path, world, kind, n_global):
     ref = O.align(full, O.make_params(algo=O.LOCAL))["score"]
     for r in range(world):
         assert np.array_equal(np.load(tmp_path / f"g{r}.npy"), ref), r
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_library_shard_bounds_match_python(world):
+    # the multi-GPU C-ABI (gasalx_shard_bounds, csrc/multi.cpp) and gasal_dist split alike
+    rng = np.random.default_rng(100 + world)
+    for n in (0, 1, 7, 1000):
+        ql = rng.integers(1, 400, n).astype(np.uint32)
+        tl = rng.integers(1, 600, n).astype(np.uint32)
+        assert G.shard_bounds(ql, tl, world) == D.shard_bounds(D.cell_counts(ql, tl), world), (n, world)
+    ql = np.full(10_000_000, 150, np.uint32)
+    tl = np.full(10_000_000, 182, np.uint32)
+    assert G.shard_bounds(ql, tl, world) == D.all_shards(10_000_000, 150, 182, world)

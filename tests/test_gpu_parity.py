@@ -553,6 +553,26 @@ def test_ksw_trimming(engine, lens, seeds):
     check(engine, b, seed=seed, algo=G.KSW, match=2, mismatch=3, gap_open=5, gap_extend=2)
 
 
+@pytest.mark.parametrize("kw", [dict(mismatch=-1), dict(mismatch=-2, match=1), dict(n_penalty=-3),
+                                dict(mismatch=-1, n_penalty=-2, match=0)])
+def test_ksw_gainful_mismatch_and_n(engine, kw):
+    # a negative mismatch (or N penalty) is a per-cell gain: the narrow entry levels must size
+    # their bound by it, not by the match score alone (h would spill into the e field)
+    rng = np.random.default_rng(len(repr(kw)))
+    b = rand_batch(int(rng.integers(1 << 16)), 1200, 100, 260, 100, 260, alphabet=b"ACGTACGTN", related=0.5)
+    seed = rng.integers(0, 40, b.n).astype(np.uint32)
+    check(engine, b, seed=seed, algo=G.KSW, **kw)
+
+
+@pytest.mark.parametrize("kw", [dict(mismatch=-1), dict(mismatch=-3, match=1), dict(n_penalty=-4),
+                                dict(mismatch=-1, n_penalty=-1, match=2)])
+def test_local_second_best_gainful_mismatch_and_n(engine, kw):
+    # local16_ok's value window counts a negative mismatch / N penalty as the per-cell gain
+    b = rand_batch(7000 + len(repr(kw)), 1500, 100, 200, 100, 240, alphabet=b"ACGTACGTN", related=0.5)
+    check(engine, b, algo=G.LOCAL, second_best=1, **kw)
+    check(engine, G.Batch.synth(2, 4001, 0x5EED0200), algo=G.LOCAL, second_best=1, **kw)
+
+
 @pytest.mark.parametrize("lds", ["0", "1"])
 @pytest.mark.parametrize("lens", [(100, 150), (400, 600), (700, 800)])
 def test_ksw_entry_storage(engine, monkeypatch, lds, lens):
