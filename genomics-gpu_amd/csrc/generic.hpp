@@ -629,8 +629,6 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     const uint32_t qoff = A.qoff[tid], toff = pk ? A.toff[tid] : 0u;
     uint4 chunk = make_uint4(0u, 0u, 0u, 0u);
     int64_t chunk_key = -1;
-    uint2 blk[4];                                    // packed layout: 2 x 2 block of chunks
-    uint32_t blk_lane = 0xFFFFFFFFu, blk_w = 0, blk_k = 0;
     uint2 qv = make_uint2(0u, 0u), tv = make_uint2(0u, 0u);
     int32_t qkey = -1, tkey = -1;
     while (i >= 0 && j >= 0) {
@@ -647,22 +645,17 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 // ((k/4)*G + lane)*4 + k%4 (wavefront16.hpp): 4 rows per 8-byte chunk
                 const uint32_t col = strip * 8 + c7;
                 const uint32_t lane = __umulhi(row, A.pk_rmagic), k = row - lane * A.pk_R;
-                const uint32_t s = col + lane, w = s >> 2, kg = k >> 2;
-                // a chunk holds 4 rows x 4 steps; the walk only moves up and left, so a
-                // miss loads the 2 x 2 block of chunks up and left of the cell at once
-                // (one round trip, four independent loads): a diagonal run then crosses
-                // a block edge every >= 5 steps instead of a chunk edge every ~2
-                if (!(lane == blk_lane && w <= blk_w && w + 1 >= blk_w && kg <= blk_k && kg + 1 >= blk_k)) {
-                    blk_lane = lane; blk_w = w; blk_k = kg;
-                    const uint16_t *c00 = tb16 + (uint64_t)w * (A.pk_G * A.pk_R) + (kg * A.pk_G + lane) * 4;
-                    const uint64_t dw = (uint64_t)A.pk_G * A.pk_R, dk = 4ull * A.pk_G;
-                    blk[0] = *reinterpret_cast<const uint2 *>(c00);
-                    blk[1] = w ? *reinterpret_cast<const uint2 *>(c00 - dw) : make_uint2(0u, 0u);
-                    blk[2] = kg ? *reinterpret_cast<const uint2 *>(c00 - dk) : make_uint2(0u, 0u);
-                    blk[3] = (w && kg) ? *reinterpret_cast<const uint2 *>(c00 - dw - dk) : make_uint2(0u, 0u);
+                const uint32_t s = col + lane;
+                // one 8-byte chunk (4 rows x 4 steps) per miss: the walk is bound by the
+                // lines it fetches (a 2 x 2 block of chunks per miss fetched 1.6x the lines
+                // and took 1.19 ms instead of 0.70, profiles/r03_tb_walk.md)
+                const int64_t key = (int64_t)(s >> 2) * (A.pk_G * A.pk_R) + ((k >> 2) * A.pk_G + lane) * 4;
+                if (key != chunk_key) {
+                    const uint2 c2 = *reinterpret_cast<const uint2 *>(tb16 + key);
+                    chunk = make_uint4(c2.x, c2.y, 0u, 0u);
+                    chunk_key = key;
                 }
-                const uint2 c2 = w == blk_w ? (kg == blk_k ? blk[0] : blk[2]) : (kg == blk_k ? blk[1] : blk[3]);
-                const uint32_t fl = (((k & 2u) ? c2.y : c2.x) >> (16 * (k & 1u) + (s & 3u))) & 0xFFFFu;
+                const uint32_t fl = (((k & 2u) ? chunk.y : chunk.x) >> (16 * (k & 1u) + (s & 3u))) & 0xFFFFu;
                 const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
                 const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
