@@ -239,3 +239,21 @@ def test_packed_value_window_edge(engine):
         al = G.NvAligner(G.NV_SW, type_, 1, -1, 0, 0, -1, -1)
         assert G.nv_describe_plan(al, 1024, 6000).startswith("nvbio16_")
         _check(engine, al, P, T)
+
+
+def test_reference_known_answers(engine):
+    # the reference's own nvbio test vectors (alignment_test.cu:680-793, as scores in
+    # tests/golden/nvbio_reference_kats.json), through the HIP kernels
+    import test_nvbio_oracle as T
+    kats = T._ref_kats()
+    for c in kats["alignment"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        # one shared text (the sw-benchmark layout), then the same text per pair
+        for shared in (True, False):
+            Tx = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False, shared=shared)
+            assert int(engine.nv_score_host(T.ref_aligner(c), P, Tx)[0]) == c["score"], (c, shared)
+    ed = kats["edit_distance"]
+    P = G.PackedSet.pack([G.dna_n_codes(c["pattern"]) for c in ed])
+    Tx = G.PackedSet.pack([G.ref2_codes(c["text"]) for c in ed], bits=2, big_endian=False)
+    got = engine.nv_score_host(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), P, Tx)
+    assert list(got) == [c["score"] for c in ed]

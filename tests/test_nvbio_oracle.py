@@ -116,3 +116,37 @@ def test_oracle_matches_textbook_dp(aligner, type_):
         P = G.PackedSet.pack([np.array(p, np.uint32)], bits=4)
         T = G.PackedSet.pack([np.array(t, np.uint32)], bits=2, big_endian=False)
         assert int(O.nv_score(al, P, T)[0]) == textbook(aligner, type_, p, t, s)
+
+
+# ---- known answers the reference's own nvbio test holds (tests/golden/nvbio_reference_kats.json,
+#      made by tests/golden/make_nvbio_reference_kats.py from alignment_test.cu:680-793) ----
+def _ref_kats():
+    import json
+    import os
+    import helpers
+    return json.load(open(os.path.join(helpers.GOLDEN, "nvbio_reference_kats.json")))
+
+
+def ref_aligner(c):
+    t = {"GLOBAL": G.NV_GLOBAL, "LOCAL": G.NV_LOCAL, "SEMI_GLOBAL": G.NV_SEMI_GLOBAL}[c["type"]]
+    s = c["scheme"]
+    if c["aligner"] == "sw":
+        return G.NvAligner(G.NV_SW, t, match=s["match"], mismatch=s["mismatch"], deletion=s["deletion"],
+                           insertion=s["insertion"])
+    return G.NvAligner(G.NV_GOTOH, t, s["match"], s["mismatch"], s["gap_open"], s["gap_ext"])
+
+
+def test_reference_alignment_test_cigars():
+    # ACAACTA vs AAACACCCTAACACACTAAA (alignment_test.cu:749-793): the optimum each expected
+    # CIGAR implies, SW and Gotoh x GLOBAL / LOCAL / SEMI_GLOBAL
+    cases = _ref_kats()["alignment"]
+    assert len(cases) == 6
+    for c in cases:
+        assert score(ref_aligner(c), c["pattern"], c["text"]) == c["score"], c
+
+
+def test_reference_edit_distance_cases():
+    # the banded (band 5) SEMI_GLOBAL edit-distance cases of alignment_test.cu:680-745 on the
+    # full DP: every stated optimum lies inside the band, so the full DP agrees
+    for c in _ref_kats()["edit_distance"]:
+        assert score(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), c["pattern"], c["text"]) == c["score"], c
