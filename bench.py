@@ -107,6 +107,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave out the all-gather of scores")
+    ap.add_argument("--force-int32", action="store_true",
+                    help="probe: every block on the int32 kernels (GASALX_PACKED16=0), as pairs outside the "
+                         "packed kernels' 16-bit value window run")
+    ap.add_argument("--scores", default="",
+                    help="probe: match,mismatch,gap_open,gap_extend overriding the workload's scores "
+                         "(e.g. 2,4,6,1 takes config 2 outside the 16-bit window)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo stages the exchange "
                          "through host memory, so several ranks can share one GPU)")
@@ -215,11 +221,24 @@ def ph_subset(h, e):
 
 
 # ---------------------------------------------------------------- oracle ----
-def _oracle():
+def _oracle(native=False):
+    """The CPU oracle.  native: its -O3 -march=native build for this host,
+    compiled here, used for the timed baseline (and the parity run that doubles as it)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
+    if native:
+        O.NATIVE = O.use_native()
     return O
+
+
+def lib_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    with open(G.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
 
 
 def oracle_threads():
@@ -474,6 +493,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     kind, pkw = wl["kind"], wl["params"]
+    probe = {}
+    if args.force_int32:
+        os.environ["GASALX_PACKED16"] = "0"
+        probe["force_int32"] = True
+    if args.scores:
+        a, b, o, e = (int(x) for x in args.scores.split(","))
+        pkw = dict(pkw or {}, match=a, mismatch=b, gap_open=o, gap_extend=e)
+        probe["scores"] = [a, b, o, e]
     per = args.pairs or wl["pairs"]
     n_global = per * world if wl["scaling"] == "weak" else per
     seed = SEEDS[kind]
@@ -635,7 +662,8 @@ def main():
 
     # ---- parity: this rank's shard against the oracle (the CPU baseline at N = 1) ----
     parity, cpu = None, None
-    O = _oracle() if (args.parity_pairs > 0 or (world == 1 and not args.no_cpu)) else None
+    O = _oracle(native=world == 1 and not args.no_cpu) if (args.parity_pairs > 0 or (world == 1 and not args.no_cpu)) \
+        else None
     threads = oracle_threads()
     if args.parity_pairs > 0:
         m = min(n, args.parity_pairs)
@@ -695,14 +723,17 @@ def main():
             cpu = {"value": round(cells_checked / oracle_s / 1e9, 4), "unit": "GCUPS", "cores": threads,
                    "kind": "port",
                    "sample": f"first {m} pairs of the rank-0 batch ({cells_checked / 1e9:.2f} G cells, "
-                             f"{oracle_s:.1f} s, the parity run), oracle/gasal_oracle.c OpenMP x{threads}"}
+                             f"{oracle_s:.1f} s, the parity run), oracle/gasal_oracle.c OpenMP x{threads}",
+                   "build": "gcc -O3 -march=native (built on this host)" if getattr(O, "NATIVE", False)
+                            else "gcc -O3 (portable build; the native build failed)"}
     if world == 1 and not args.no_cpu:
         if cpu is None:
             cpu = {"value": None, "unit": "GCUPS", "cores": threads, "kind": "port", "sample": "parity run skipped"}
         cpu["single_core"] = single_core_rate(O, kind, data, pkw, args.cpu_seconds)
         cpu["host"] = host_info()
         cpu["note"] = (f"cores = the OpenMP threads used (OMP_NUM_THREADS, else min(16, CPUs)): one GPU's "
-                       f"CPU share on this pool; host totals in 'host'")
+                       f"CPU share on this pool, which limits a job's worker pool to it; host totals in "
+                       f"'host' (the whole machine's CPUs, shared by its 8 GPUs' jobs, are not timed)")
 
     if rank == 0:
         total_cells = n_global * rl * hl        # every pair of every shard (uniform lengths)
@@ -716,7 +747,11 @@ def main():
                 pmc = json.load(open(pmc_path))
             except Exception:
                 pmc = None
-        same = pmc is not None and pmc.get("pairs_per_launch") == n
+        # counters only from a pass over this very build and plan (the library's sha256 changes
+        # with any kernel change, so a stale file is never used); otherwise traffic is null
+        sha = lib_sha256()
+        same = (pmc is not None and pmc.get("pairs_per_launch") == n and pmc.get("plan") == plan and
+                pmc.get("lib_sha256") == sha and not probe)
         traffic = pmc.get("hbm_bytes_per_launch") if same else None
         packed = plan.startswith(("wavefront16", "nvbio16"))
         lane_rate = VALU_LANE_OPS * (2 if packed else 1)
@@ -750,10 +785,17 @@ def main():
                              "(banded.h:35,73-75) at the " + ("packed 2x16-bit" if rate > VALU_LANE_OPS else "int32") +
                              f" VALU lane rate {rate / 1e12:.1f} T ops/s"}
         if same and pmc.get("valu_insts_per_launch"):
+            # issue-slot use: VALU issue cycles of the dominant kernel (SQ_ACTIVE_INST_VALU counts
+            # quad-cycles, MI355X_MICROARCH.md) over the SIMD-cycles of its launch at 2.4 GHz
+            pk_t = pmc.get("kernel_ns", 0) / 1e9 or kern_s
+            act = pmc.get("counters", {}).get("SQ_ACTIVE_INST_VALU")
             valu["issue"] = {"valu_wave_instr_per_launch": pmc["valu_insts_per_launch"],
                              "cycles_per_valu_instr_per_simd":
-                                 round(SIMDS * CLOCK * kern_s / pmc["valu_insts_per_launch"], 3),
-                             "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU)"}
+                                 round(SIMDS * CLOCK * pk_t / pmc["valu_insts_per_launch"], 3),
+                             "issue_slot_use": round(4 * act / (SIMDS * CLOCK * pk_t), 4) if act else None,
+                             "kernel": pmc.get("kernel"),
+                             "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU; "
+                                       f"same library sha256 and plan as this run)"}
         out = {
             "metric": METRICS.get(args.workload, MAIN_METRIC),
             "value": round(gcups, 2),
@@ -768,7 +810,8 @@ def main():
             "dtype": dtype_label(plan, kind),
             "data": "synthetic (SURVEY.md 8(d) generator), resident in HBM",
             "config": {"workload": wl["label"], "pairs_global": n_global, "pairs_rank0": n,
-                       "cells_rank0_step": cells_per_step, "plan": plan,
+                       "cells_rank0_step": cells_per_step, "plan": plan, "lib_sha256": sha,
+                       **({"probe": probe} if probe else {}),
                        "parallelism": f"dp{world} (cell-balanced contiguous shards of one global batch)" +
                                       ((", RCCL all-gather of scores in every step" if backend == "nccl" else
                                         ", gloo all-gather of scores (through host memory) in every step")

@@ -245,7 +245,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         pl.kind = PLAN_WAVEFRONT;
         pl.wf_algo = wf_algo; pl.keys = keys; pl.tb = tb && wf_algo != WF_SEMI;
         pl.need_pack = has_ops;
-        pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin);
+        // GASALX_PACKED16=0: every block on the int32 kernel (A/B runs, the int32 probe of
+        // bench.py --force-int32); read per call
+        const char *pk_env = std::getenv("GASALX_PACKED16");
+        pl.packed16 = !(pk_env && std::atoi(pk_env) == 0) && packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin);
         if (pl.packed16) {
             const uint32_t x8 = (wf_algo == WF_SEMI) ? t8 : q8, y8 = (wf_algo == WF_SEMI) ? q8 : t8;
             pl.G16 = 0;

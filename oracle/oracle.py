@@ -35,6 +35,21 @@ def build() -> str:
     return _LIB_PATH
 
 
+def use_native() -> bool:
+    """Switch this process to the -O3 -march=native build (oracle/Makefile `native`),
+    compiled here for this host's CPU: the timed CPU baseline of bench.py.  Must be
+    called before the first oracle call.  False (portable build kept) if it fails."""
+    global _LIB_PATH
+    if _lib is not None:
+        return _LIB_PATH.endswith(os.path.join("native", "liborc.so"))
+    try:
+        subprocess.run(["make", "-s", "-C", _HERE, "native"], check=True, capture_output=True, timeout=300)
+    except Exception:
+        return False
+    _LIB_PATH = os.path.join(_HERE, "build", "native", "liborc.so")
+    return True
+
+
 def lib():
     global _lib
     if _lib is None:

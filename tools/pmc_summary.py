@@ -7,6 +7,8 @@ For the dominant kernel of the bench step (its longest dispatch), records every 
                            FETCH_SIZE tallies 128-B requests at 64 B, see
                            MI355X_MICROARCH.md, HBM section)
   valu_insts_per_launch  = SQ_INSTS_VALU (wave instructions)
+plus the plan and libgasal sha256 the passes ran (bench.py uses the file only for the
+same build and plan) and the dominant dispatch's duration (kernel_ns).
 """
 import collections
 import csv
@@ -44,6 +46,17 @@ def main(run_dir, workload, pairs):
     best = max(per, key=lambda k: max(v for (kk, _), v in dur.items() if kk == k))
     c = per[best]
     out = {"workload": workload, "kernel": best, "pairs_per_launch": int(pairs), "counters": c}
+    # the bench lines the passes printed: their plan and library hash (bench.py accepts this
+    # file only for a run of the same build and plan)
+    for path in sorted(glob.glob(os.path.join(run_dir, "p*.json"))):
+        try:
+            line = [ln for ln in open(path) if ln.startswith("{")][-1]
+            cfg = json.loads(line)["config"]
+            out["plan"], out["lib_sha256"] = cfg.get("plan"), cfg.get("lib_sha256")
+            break
+        except Exception:
+            continue
+    out["kernel_ns"] = min(v for (kk, _), v in dur.items() if kk == best)
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         out["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
     if "SQ_INSTS_VALU" in c:
