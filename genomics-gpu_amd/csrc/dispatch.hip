@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "banded16.hpp"
 #include "local16.hpp"
@@ -142,7 +143,11 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
     }
     int64_t k, top, drift = 0;
     if (wf_algo == WF_SEMI) {
-        if (p.tail != 2) return false;                         // TAIL=TARGET only (last query row)
+        // TAIL=TARGET (last query row); TAIL=QUERY/BOTH score-only through the class launches
+        // (the last padded column, Q11): targets up to 256 (R <= 32), rows keyed in 16 bits
+        const bool tq = p.start_pos == 0 && (p.tail == 1 || p.tail == 3);
+        if (p.tail != 2 && !tq) return false;
+        if (tq && (t8 > 256 || q8 > 65535)) return false;
         if (oe < b || oe < npen) return false;                 // table offset K = OE
         k = oe;
     } else {
@@ -227,6 +232,13 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         wf_algo = WF_SEMI;
         keys = (p.tail == 2 || p.tail == 3);
     }
+    // SEMI TAIL=NONE, score-only: the reference keeps maxHH = MINUS_INF and the initial ends
+    // (semiglobal_kernel_template.h:49-51,63-64,206-218; neither tail block runs)
+    if (p.algo == 2 && p.tail == 0 && p.start_pos == 0 && !p.second_best) {
+        pl.kind = PLAN_CONST;
+        pl.name = "semi_tail_none";
+        return pl;
+    }
     bool ok = wf_algo >= 0 && int16_safe(p, s.max_q, s.max_t) && t8 < 32000 && p.gap_extend >= 0;
     if (wf_algo == WF_SEMI && p.start_pos == 1 && t8 > 8192) ok = false;   // stop key: strips < 1024
     if (ok) {
@@ -271,6 +283,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                     pl.G16 = sh.G; pl.R16 = sh.R;
                     break;
                 }
+            // SEMI TAIL=QUERY/BOTH: G = 8 and R = padded target / 8 per class launch (the
+            // last padded column at register R - 1 of lane 7); the plan names the largest
+            pl.semi_tq = pl.packed16 && wf_algo == WF_SEMI && p.tail != 2;
+            if (pl.semi_tq) { pl.G16 = 8; pl.R16 = (int)(x8 / 8); }
             const uint32_t words = (y8 + 2 * pl.G16 + 4 + 3) & ~3u;   // odd-step tail + prefetch
             pl.lds16_stride = words * 8;                               // uint2 per position
             pl.lds16_bytes = (size_t)kWavesPerBlock * (64 / std::max(pl.G16, 1)) * pl.lds16_stride;
@@ -279,9 +295,11 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin,
                                           (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8);
             pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
+            pl.semi_tq = pl.semi_tq && pl.packed16;
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
-                       : wf_algo == WF_GLOBAL ? "global" : (p.start_pos == 1 ? "semi_start" : "semi");
+                       : wf_algo == WF_GLOBAL ? "global"
+                       : pl.semi_tq ? "semi_tq" : (p.start_pos == 1 ? "semi_start" : "semi");
         if (pl.packed16)
             pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + (pl.key2 ? "_k2" : "") + "_G" + std::to_string(pl.G16) + "R" +
                       std::to_string(pl.R16);
@@ -365,6 +383,86 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
     hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
+}
+
+// SEMI TAIL=QUERY/BOTH, packed (wavefront16.hpp WF16_SEMI_TQ): one launch per class of
+// pairs with the same padded target length 8R, over a slot range (slots sorted by target
+// words when the batch holds more than one class; the class sizes are read back, one
+// synchronisation of the stream), flags per slot; then the int32 kernel over the slots
+// the packed launches declined.
+static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p, const WfArgs &base,
+                          hipStream_t st) {
+    WfArgs A = base;
+    const uint32_t n = A.n;
+    A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
+    A.nval = p.n_code & 0xF;
+    A.has_npen = p.has_n_penalty; A.npen = p.n_penalty;
+    A.head = p.head; A.tail = p.tail;
+    A.lds_stride = pl.lds_stride;
+    A.force_exact = (p.mismatch <= 0 || (p.has_n_penalty && p.n_penalty < 0)) ? 1 : 0;
+    A.one = 0x00010001u;
+    const uint32_t t8w = (uint32_t)pl.R16;                  // largest class
+    const size_t sh = (size_t)(t8w + 1) * 4;
+    HIPCHK(ws.sort_meta.reserve((size_t)n * 4 + 2 * sh + 64));
+    uint32_t *perm = ws.sort_meta.as<uint32_t>(), *hist = perm + n, *cursor = hist + t8w + 1;
+    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, hist);
+    HIPCHK(hipGetLastError());
+    std::vector<uint32_t> h(t8w + 1);
+    HIPCHK(hipMemcpyAsync(h.data(), hist, sh, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int classes = 0;
+    for (uint32_t b = 0; b <= t8w; b++) classes += h[b] != 0;
+    A.perm = nullptr;
+    if (classes > 1) {                                       // counting sort: longest targets first
+        rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
+        rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, cursor, perm);
+        HIPCHK(hipGetLastError());
+        A.perm = perm;
+    }
+    HIPCHK(ws.misc.reserve(n + 64));
+    HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));            // slots no class launch covers stay declined
+    WfArgs P16 = A;
+    P16.lds_stride = pl.lds16_stride;
+    P16.fast16 = 1;
+    P16.vmin = pl.vmin;
+    P16.handled = ws.misc.as<uint8_t>();
+    const uint32_t ppb16 = kWavesPerBlock * (64 / 8) * 2;
+    uint32_t slot = 0;
+    for (uint32_t b = 0; b <= t8w; slot += h[b], b++) {
+        const uint32_t R = t8w - b;                          // bucket b: padded target of 8R
+        if (!h[b] || R == 0) continue;
+        Wf16Fn fn = wf16_tq_lookup((int)R);
+        if (!fn) { set_error("no packed TAIL=QUERY/BOTH instance"); return GASALX_EUNSUPPORTED; }
+        if (pl.lds16_bytes > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)pl.lds16_bytes));
+        P16.slot0 = slot;
+        P16.n = slot + h[b];
+        hipLaunchKernelGGL(fn, dim3(grid_for(h[b], ppb16)), dim3(kBlock), pl.lds16_bytes, st, P16);
+        HIPCHK(hipGetLastError());
+    }
+    A.skip = ws.misc.as<uint8_t>();
+    A.skip_ppb = 1;
+    WfFn fn = wf_lookup(pl.wf_algo, pl.keys, false, pl.G, pl.R);
+    if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
+    if (pl.lds_bytes > 64 * 1024)
+        HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
+    hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
+    HIPCHK(hipGetLastError());
+    return GASALX_OK;
+}
+
+// SEMI TAIL=NONE outputs (PLAN_CONST): score MINUS_INF, query_batch_end = maxXY_x =
+// ref_len, target_batch_end = maxXY_y = read_len (semiglobal_kernel_template.h:49-51,63-64,
+// 206-218: Q10's end conventions with no tail block run)
+__global__ __launch_bounds__(256) void semi_tail_none_kernel(int32_t *score, int32_t *qend, int32_t *tend,
+                                                             const uint32_t *qlen, const uint32_t *tlen, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    score[i] = -32768;
+    if (qend) qend[i] = (int32_t)tlen[i];
+    if (tend) tend[i] = (int32_t)qlen[i];
 }
 
 // WITH_START on the wavefront kernels (start.hpp): reversed slots sorted by
@@ -570,6 +668,12 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
     const uint32_t n = b.n_alns;
     const bool tb = p.start_pos == 2;
     const bool runs_tb = tb && (p.algo == 1 || p.algo == 3) && pl.kind != PLAN_NONE;
+    if (pl.kind == PLAN_CONST) {
+        if (dp) semi_tail_none_kernel<<<grid_for(n, 256), 256, 0, st>>>(out.aln_score, out.q_end, out.t_end, b.q_lens,
+                                                                      b.t_lens, n);
+        HIPCHK(hipGetLastError());
+        return GASALX_OK;
+    }
 
     const uint8_t *qsrc = b.q_batch, *tsrc = b.t_batch;
     int packed = p.is_packed ? 1 : 0;
@@ -633,7 +737,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         // uneven lengths: a wave's step count is set by its longest step-axis
         // sequence (target; query for the transposed SEMI kernel), so run the
         // slots in length order (counting sort, longest first)
-        if (sort_wanted(shape) && n >= 4096) {
+        if (sort_wanted(shape) && n >= 4096 && !pl.semi_tq) {   // (semi_tq sorts by target class itself)
             const uint32_t s8w = pad8(pl.wf_algo == WF_SEMI ? shape.max_q : shape.max_t) / 8;
             const uint32_t *slen = pl.wf_algo == WF_SEMI ? b.q_lens : b.t_lens;
             const size_t sh = (size_t)(s8w + 1) * 4;
@@ -652,7 +756,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                 slot_of = inv;
             }
         }
-        int rc = dp ? launch_wavefront(ws, pl, p, A, st) : GASALX_OK;
+        int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start && dp) {
             if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {

@@ -43,7 +43,8 @@ struct Workspace {
     void release_all();
 };
 
-enum PlanKind { PLAN_NONE = 0, PLAN_WAVEFRONT, PLAN_GENERIC };
+// PLAN_CONST: outputs that do not depend on the DP (SEMI TAIL=NONE, score-only)
+enum PlanKind { PLAN_NONE = 0, PLAN_WAVEFRONT, PLAN_GENERIC, PLAN_CONST };
 
 struct Plan {
     PlanKind kind = PLAN_NONE;
@@ -61,6 +62,7 @@ struct Plan {
     bool need_pack = false; // generic kernels / reverse-complement need packed words
     bool band16 = false;    // banded: two pairs per lane in 16-bit halves (banded16.hpp), int32 fallback
     bool local16 = false;   // LOCAL second best: two pairs per lane in 16-bit halves (local16.hpp), int32 fallback
+    bool semi_tq = false;   // SEMI TAIL=QUERY/BOTH: packed class launches (one per padded target length), int32 fallback
     std::string name;
 };
 

@@ -303,14 +303,19 @@ __device__ __forceinline__ void step_local_tb(const uint2 T, const int32_t c, co
 // Stored values are H - OE ("Hm").  In: diag_top = Hm(r-1, c0-1),
 // hl/el = Hm(r, c0-1) / E(r, c0-1) entering the lane's first column.
 // ---------------------------------------------------------------------------
-template <int R>
+// PV > 0 (TAIL=QUERY/BOTH kernel): the last PV registers may hold pad columns of the
+// target, which the reference scores by its N rule (Q6/Q7, read by Q11); their selector
+// picks the constant 0 and pv adds the N score + OE per half (0 for real columns).
+template <int R, int PV = 0>
 __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top, uint32_t &hl, uint32_t &el,
                                           const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
-                                          uint32_t (&Fk)[R], const uint32_t OE, const uint32_t EXT) {
+                                          uint32_t (&Fk)[R], const uint32_t OE, const uint32_t EXT,
+                                          const uint32_t *pv = nullptr) {
     uint32_t diag = diag_top, h = hl, e = el;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        if (PV > 0 && k >= R - PV) v = pk_addnc(v, pv[k - (R - PV)]);
         const uint32_t tmp = pk_addnc(diag, v);                     // H(r-1,c-1) + s
         Fk[k] = pk_max_u16(Hin[k], pk_subnb(Fk[k], EXT));            // F(r,c)
         e = pk_max_u16(h, pk_subnb(e, EXT));                         // E(r,c)
@@ -328,21 +333,31 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
 constexpr int WF16_LOCAL_TB = 4;      // LOCAL with traceback words (wavefront16 only)
 constexpr int WF16_LOCAL_K2 = 5;      // LOCAL, padded targets of 257..512 columns (two keys per row)
+constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last padded column's rows (Q11)
+#ifndef GX_WF16_TQ_WAVES
+#define GX_WF16_TQ_WAVES 3
+#endif
 
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                    : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
-                                   : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
+                                   : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES
+                                   : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? 2 : GX_WF16_TQ_WAVES)   // R > 20 spills at 3
+                                   : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
-    constexpr int ALGO = GTB ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : ALGO_;
+    // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
+    // last padded column is always register R - 1 of lane G - 1
+    constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
+    static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
+    constexpr int ALGO = GTB ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : TQ ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1), slot = lane / G;
-    const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * (2 * S);
+    const uint32_t pair0 = (TQ ? A.slot0 : 0u) + (blockIdx.x * kWavesPerBlock + wave) * (2 * S);
     uint32_t pr[2], xl[2], yl[2], xo[2], yo[2], xpad[2], ypad[2];
     bool valid[2];
     const uint8_t *X = TR ? A.t : A.q, *Y = TR ? A.q : A.t;
@@ -421,14 +436,38 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T
                     xs[k] = (xs[k] & ~(0xFFu << (16 * h))) | ((l + 4 * h) << (16 * h));
-                } else if (ALGO == WF_LOCAL || GTB) {
-                    other |= l != 4;                 // pads must be N (LOCAL: scored -K here, dominated)
-                }
+                } else if (ALGO == WF_LOCAL || GTB || TQ) {
+                    other |= l != 4;                 // pads must be N (LOCAL: scored -K here, dominated;
+                }                                    // TQ: scored by the N rule through pv)
             }
         }
     }
+    // TQ: pad columns sit in the last PV registers (of the last lanes); their N-rule score
+    constexpr int PV = TQ ? (R < 7 ? R : 7) : 0;
+    uint32_t pv[PV > 0 ? PV : 1];
+    if constexpr (TQ) {
+        const int32_t nrule = A.has_npen ? -A.npen : 0;   // gasal_kernels.h:44-51 LOCAL macro (semi-global uses it)
+#pragma unroll
+        for (int j = 0; j < PV; ++j) {
+            const uint32_t r = r0 + (R - PV) + j;
+            pv[j] = 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (valid[h] && r >= xl[h] && r < xpad[h]) pv[j] |= (uint32_t)(nrule + A.o + A.e) << (16 * h);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) other |= valid[h] && xpad[h] != (uint32_t)(G * R);   // the launch's class
+    }
     const bool fast = A.fast16 && !A.force_exact && !__syncthreads_or(other);
-    if (threadIdx.x == 0) A.handled[blockIdx.x] = fast ? 1 : 0;
+    if constexpr (TQ) {
+        // flags per slot: class launches cover slot ranges that need not align to blocks
+        if (lg == 0)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (valid[h]) A.handled[pair0 + 2 * slot + h] = fast ? 1 : 0;
+    } else if (threadIdx.x == 0) {
+        A.handled[blockIdx.x] = fast ? 1 : 0;
+    }
     if (!fast) return;                                   // the int32 kernel takes this block
 
     const uint32_t nsteps = ymaxw + G - 1;
@@ -784,6 +823,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // Reverse pass (A.stop, start.hpp): values >= the forward score rank first,
         // by smallest 8-column strip, then value, then first column (bit 31 set).
         uint32_t best[2] = {0, 0};
+        uint32_t bestq[2] = {0, 0};                     // TQ: key (H, -row) of the last padded column
+        const bool tail_t = !TQ || A.tail == 3;         // the last-row maximum (TAIL TARGET / BOTH)
         int32_t thrp[2] = {0x7FFFFFFF, 0x7FFFFFFF};
         if (A.stop) {
 #pragma unroll
@@ -807,10 +848,21 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             } else {
                 hl = top ? hleft(cc) : recvH;
                 el = top ? eleft : recvE;
-                step_semi<R>(T, top ? hleft(cc - 1) : prevRecvH, hl, el, xs, Hin, Hout, Fk, OE, EXT);
+                step_semi<R, PV>(T, top ? hleft(cc - 1) : prevRecvH, hl, el, xs, Hin, Hout, Fk, OE, EXT, pv);
+                if constexpr (TQ) {
+                    // semiglobal :185-193 (Q11): H of row cc at the last padded column, which is
+                    // register R - 1 of lane G - 1 (the other lanes' keys are never read);
+                    // the largest key is the first row of the maximum
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const uint32_t v = (Hout[R - 1] >> (16 * h)) & 0xFFFFu;
+                        const uint32_t cand = (uint32_t)cc < yl[h] ? (v << 16) | (0xFFFFu - (uint32_t)cc) : 0u;
+                        bestq[h] = cand > bestq[h] ? cand : bestq[h];
+                    }
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    if (valid[h] && cc == (int32_t)yl[h] - 1) {                 // semiglobal :160-178
+                    if (tail_t && valid[h] && cc == (int32_t)yl[h] - 1) {       // semiglobal :160-178
 #pragma unroll
                         for (int k = 0; k < R; ++k) {
                             const uint32_t col = r0 + k;
@@ -838,6 +890,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             uint32_t b = best[h];
 #pragma unroll
             for (int m = 1; m < G; m <<= 1) b = max(b, (uint32_t)__shfl_xor(b, m));
+            const uint32_t bq = TQ ? (uint32_t)__shfl(bestq[h], (int)(slot * G + G - 1)) : 0u;
             if (valid[h] && lg == 0) {
                 // semiglobal :49,63-64,206-218 (Q10): q_end = tl, t_end = column of the max
                 int32_t score = -32768, qe = (int32_t)xl[h], te = (int32_t)yl[h];
@@ -848,6 +901,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     score = (int32_t)(b >> 16) - pb + oe;
                     te = (int32_t)(0xFFFFu - (b & 0xFFFFu));
                 }
+                if (TQ && bq != 0) {
+                    // :185-203: a row of the last padded column strictly above the maximum so
+                    // far moves the end to (row, ...); then t_end = ql unless that row is tl
+                    const int32_t vq = (int32_t)(bq >> 16) - pb + oe;
+                    if (vq > score) { score = vq; qe = (int32_t)(0xFFFFu - (bq & 0xFFFFu)); }
+                }
+                if (TQ && qe != (int32_t)xl[h]) te = (int32_t)yl[h];
                 A.score[pr[h]] = score;
                 if (A.qend) A.qend[pr[h]] = qe;
                 if (A.tend) A.tend[pr[h]] = te;
@@ -855,5 +915,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         }
     }
 }
+
+// SEMI TAIL=QUERY/BOTH instances, G = 8, R = 1..32 (semi_tq.hip; one per padded target
+// length 8R): NULL outside that range
+using Wf16Fn = void (*)(WfArgs);
+Wf16Fn wf16_tq_lookup(int R);
 
 }  // namespace gx

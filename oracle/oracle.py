@@ -15,7 +15,6 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liborc.so")
-_lib = None
 
 # enum values of the reference (gasal.h:37-73)
 WITHOUT_START, WITH_START, WITH_TB = 0, 1, 2
@@ -35,30 +34,41 @@ def build() -> str:
     return _LIB_PATH
 
 
-def use_native() -> bool:
-    """Switch this process to the -O3 -march=native build (oracle/Makefile `native`),
-    compiled here for this host's CPU: the timed CPU baseline of bench.py.  Must be
-    called before the first oracle call.  False (portable build kept) if it fails."""
-    global _LIB_PATH
-    if _lib is not None:
-        return _LIB_PATH.endswith(os.path.join("native", "liborc.so"))
+_NATIVE_PATH = os.path.join(_HERE, "build", "native", "liborc.so")
+_libs = {}            # path -> loaded handle
+_active = None        # path lib() returns (None: the portable build)
+
+
+def native_available() -> bool:
+    """Build the -O3 -march=native variant (oracle/Makefile `native`) for this host's CPU:
+    the timed CPU baseline of bench.py.  False if it does not build."""
     try:
         subprocess.run(["make", "-s", "-C", _HERE, "native"], check=True, capture_output=True, timeout=300)
     except Exception:
         return False
-    _LIB_PATH = os.path.join(_HERE, "build", "native", "liborc.so")
-    return True
+    return os.path.exists(_NATIVE_PATH)
+
+
+def use_native(on: bool = True) -> bool:
+    """Route the oracle calls of this process through the native (on) or the portable
+    build; both stay loaded.  Returns whether the native build is now in use."""
+    global _active
+    if on and not native_available():
+        on = False
+    _active = _NATIVE_PATH if on else None
+    return on
 
 
 def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+    path = _active or _LIB_PATH
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
-        _lib = ctypes.CDLL(_LIB_PATH)
-        _lib.orc_aln_batch.restype = ctypes.c_int
-        _lib.orc_pairhmm_batch.restype = ctypes.c_int
-    return _lib
+        h = ctypes.CDLL(path)
+        h.orc_aln_batch.restype = ctypes.c_int
+        h.orc_pairhmm_batch.restype = ctypes.c_int
+        _libs[path] = h
+    return _libs[path]
 
 
 def _ptr(a):

@@ -1075,3 +1075,96 @@ def test_host_pipeline_cigar_overflow_at_chunk_edge(engine):
         off = int(b.q_offsets[k])
         if not np.array_equal(g["cigar"][off:off + m], o["cigar"][off:off + m]):
             raise AssertionError(f"pair {k}: own-slot CIGAR bytes differ")
+
+
+# ------------------------------------------ SEMI TAIL = QUERY / BOTH / NONE ----
+# semiglobal_kernel_template.h:160-203: TAIL=QUERY reads H at the last padded target
+# column (Q11) for every query row, TAIL=BOTH after the last-row maximum, and the end
+# rule "t_end = ql unless q_end == tl"; TAIL=NONE writes MINUS_INF and the initial ends.
+# The packed kernel (wavefront16.hpp WF16_SEMI_TQ) runs one launch per padded target
+# length 8R (dispatch.hip launch_semi_tq), the pad columns scored by the N rule.
+TQ_TAILS = [G.QUERY, G.BOTH]
+
+
+def test_semiglobal_every_head_tail_plan():
+    for head in (G.NONE, G.QUERY, G.TARGET, G.BOTH):
+        for tail in (G.NONE, G.QUERY, G.TARGET, G.BOTH):
+            name = G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL, head=head, tail=tail), 150, 182)
+            want = {G.NONE: "semi_tail_none", G.TARGET: "wavefront16_semi_G8R23"}.get(tail, "wavefront16_semi_tq_G8R23")
+            assert name == want, (head, tail, name)
+
+
+@pytest.mark.parametrize("tail", TQ_TAILS)
+@pytest.mark.parametrize("head", [G.NONE, G.QUERY, G.TARGET, G.BOTH])
+def test_semiglobal_tail_query_config4(engine, head, tail):
+    # one class (182 bp windows: 184 padded, R = 23, two pad columns), every score set
+    b = G.Batch.synth(4, 3000, 0x5EED0400 + 4 * head + tail)
+    for a, bb, o, e in SEMI_SCORES:
+        check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+
+
+@pytest.mark.parametrize("tail", TQ_TAILS)
+@pytest.mark.parametrize("head", [G.NONE, G.QUERY, G.TARGET, G.BOTH])
+def test_semiglobal_tail_query_classes(engine, head, tail):
+    # targets of 1..256 (every class R = 1..32, a length-sorted slot order), queries shorter
+    # and longer than their targets (rows past tl: the q_end == tl end rule), 0..7 pad columns
+    rng = np.random.default_rng(0x7A11 + 4 * head + tail)
+    qs, ts = [], []
+    for i in range(2500):
+        tl = int(rng.integers(1, 257))
+        ql = int(rng.integers(1, min(3 * tl, 400) + 1))
+        t = helpers.random_seq(rng, tl)
+        q = (helpers.mutate(rng, t * 3)[:ql] if i % 2 else helpers.random_seq(rng, ql))
+        qs.append(q); ts.append(t)
+    b = G.Batch.from_pairs(qs, ts)
+    assert G.describe_plan(G.make_params(algo=G.SEMI_GLOBAL, head=head, tail=tail), 400, 256) == \
+        "wavefront16_semi_tq_G8R32"
+    check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail)
+    check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, match=2, mismatch=3, gap_open=5, gap_extend=2)
+
+
+@pytest.mark.parametrize("tail", TQ_TAILS)
+@pytest.mark.parametrize("npen", [None, 2, 0])
+def test_semiglobal_tail_query_n_and_iupac(engine, tail, npen):
+    # N in targets and queries (the N rule, with and without N_PENALTY), other letters:
+    # blocks holding them are declined per slot to the int32 kernel
+    rng = np.random.default_rng(0x7A20 + tail * 3 + (npen or 0))
+    qs, ts = helpers.random_pairs(rng, 2000, 1, 200, 1, 250, alphabet=b"ACGTACGTACGTN")
+    qs[7] = qs[7][:3] + b"R" + qs[7][4:]
+    b = G.Batch.from_pairs(qs, ts)
+    for head in (G.NONE, G.BOTH):
+        check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, n_penalty=npen)
+
+
+def test_semiglobal_tail_query_ties_and_rows_past_target(engine):
+    # a query that repeats the target: the last column's maximum recurs on later rows
+    # (first row wins), rows at index tl and beyond, equal target-row and column maxima
+    qs, ts = [], []
+    for t in (b"ACGTACGTAC", b"ACGTACGT", b"AAAAAAAAAAAAAAAA", b"ACG", b"A"):
+        for k in (1, 2, 3, 5):
+            qs.append(t * k)
+            ts.append(t)
+            qs.append((t * k)[1:])
+            ts.append(t)
+    b = G.Batch.from_pairs(qs, ts)
+    for head in (G.NONE, G.QUERY, G.TARGET, G.BOTH):
+        for tail in TQ_TAILS:
+            check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail)
+
+
+def test_semiglobal_tail_none_outputs(engine):
+    b = rand_batch(0x7A30, 777, 1, 300, 1, 300)
+    for head in (G.NONE, G.QUERY, G.TARGET, G.BOTH):
+        g, _ = check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=G.NONE)
+        assert (g["score"] == -32768).all() and np.array_equal(g["q_end"], b.t_lens.astype(np.int32))
+
+
+def test_semiglobal_tail_query_equals_int32_kernel(engine, monkeypatch):
+    b = G.Batch.synth(4, 20000, 0x5EED0004)
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.BOTH)
+    r16 = engine.align_host(b, G.make_params(**kw))
+    monkeypatch.setenv("GASALX_PACKED16", "0")
+    assert G.describe_plan(G.make_params(**kw), 150, 182).startswith("wavefront_semi")
+    r32 = engine.align_host(b, G.make_params(**kw))
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(r16[f], r32[f]), f

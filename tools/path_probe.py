@@ -30,6 +30,8 @@ MODES = [
     ("semi_tt_start", 4, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
                               max_query_len=192)),
     ("semi_both", 4, dict(algo=G.SEMI_GLOBAL, head=G.BOTH, tail=G.BOTH)),
+    ("semi_query", 4, dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.QUERY)),
+    ("semi_none", 4, dict(algo=G.SEMI_GLOBAL, head=G.NONE, tail=G.NONE)),
     ("global", 3, dict(algo=G.GLOBAL)),
     ("global_tb", 3, dict(algo=G.GLOBAL, start_pos=G.WITH_TB)),
     ("banded16", 2, dict(algo=G.BANDED, k_band=16)),
