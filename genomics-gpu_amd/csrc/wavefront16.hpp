@@ -337,12 +337,15 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
+#ifndef GX_WF16_TQ_BIG_WAVES
+#define GX_WF16_TQ_BIG_WAVES 3   // R > 20 (A/B knob): 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
+#endif
 
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                    : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
                                    : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES
-                                   : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? 2 : GX_WF16_TQ_WAVES)   // R > 20 spills at 3
+                                   : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? GX_WF16_TQ_BIG_WAVES : GX_WF16_TQ_WAVES)
                                    : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
