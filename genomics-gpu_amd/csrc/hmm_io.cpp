@@ -85,6 +85,9 @@ int gasalx_hmm_file_read(const char *path, gasalx_hmm_file **out) {
             long rl, hl, q;
             if (!t.integer(&rl) || rl <= 0) return fail("bad read length");
             if (!t.next() || (long)t.tok.size() < rl) return fail("read shorter than its length");
+            // offsets are uint32 (gasalx_hmm_file): a file past 4 GiB of read (or haplotype)
+            // bytes is refused rather than wrapped
+            if (reads.size() + (uint64_t)rl > 0xFFFFFFFFull) return fail("more than 4 GiB of read bases");
             roff.push_back((uint32_t)reads.size());
             rlen.push_back((uint32_t)rl);
             reads.insert(reads.end(), t.tok.begin(), t.tok.begin() + rl);
@@ -95,6 +98,7 @@ int gasalx_hmm_file_read(const char *path, gasalx_hmm_file **out) {
                 }
             if (!t.integer(&hl) || hl <= 0) return fail("bad haplotype length");
             if (!t.next() || (long)t.tok.size() < hl) return fail("haplotype shorter than its length");
+            if (haps.size() + (uint64_t)hl > 0xFFFFFFFFull) return fail("more than 4 GiB of haplotype bases");
             hoff.push_back((uint32_t)haps.size());
             hlen.push_back((uint32_t)hl);
             haps.insert(haps.end(), t.tok.begin(), t.tok.begin() + hl);

@@ -618,7 +618,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         uint32_t kq_lane[2], kq[2], kp_lane[2], kp[2];
         bool fixable[2];
         int32_t score[2] = {0, 0}, fixv[2] = {0, 0};
-        uint32_t capq[2] = {0, 0}, capp[2] = {0, 0};   // GX_WF16_CAPTURE_TREE: the captured registers
+#if GX_WF16_CAPTURE_TREE
+        uint32_t capq[2] = {0, 0}, capp[2] = {0, 0};   // the captured registers
+#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             kq_lane[h] = (xl[h] - 1) / R;
