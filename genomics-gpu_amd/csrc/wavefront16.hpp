@@ -207,12 +207,24 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 // bit2 = E extended, bit3 = F extended; here each cell records four "differs"
 // flags and tb_kernel rebuilds the nibble (s < 0 it takes from the sequences):
 //   u = [H != tmp], w = [H != F], x = [toe > E - e], y = [toe > F - e]
-// (x, y are the reference's own "not extended" tests).  A flag is bit 15 of
-// (A + 0x7FFF) - B: [A != B] for A >= B, [A > B] for |A - B| < 0x7800, and no
-// carry/borrow crosses a half either way; v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
+// (x, y are the reference's own "not extended" tests).  A flag is bit 15 of the
+// per-half difference B - A (one v_pk_sub_u16): [A != B] for A >= B, [A > B] for
+// |A - B| < 0x7800 (GX_TB_FLAG_ADD 1: the round-2 form, (A + 0x7FFF) - B as two
+// 32-bit ops with no carry/borrow across a half, 6 instructions for 4 flags instead
+// of 4); v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
 // v_and_or places them: step j of a 4-step window owns bits j (u), 4+j (w),
 // 8+j (x) and 12+j (y) of each 16-bit half of dw.
 // ---------------------------------------------------------------------------
+#ifndef GX_TB_FLAG_ADD
+#define GX_TB_FLAG_ADD 0
+#endif
+__device__ __forceinline__ uint32_t tb_flag(uint32_t a, uint32_t b) {
+#if GX_TB_FLAG_ADD
+    return (a + 0x7FFF7FFFu) - b;
+#else
+    return GX_AS(uint32_t, GX_AS(pk_u2, b) - GX_AS(pk_u2, a));
+#endif
+}
 // (a & m) | b as one v_bitop3_b32 (truth table 0xEA); the compiler would
 // otherwise split the two merges of a row into and, and, or3
 __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
@@ -225,7 +237,6 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
                                                uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
                                                uint32_t &f_out, const uint32_t OED, const uint32_t EXT,
                                                const uint32_t NN, const int j) {
-    constexpr uint32_t C = 0x7FFF7FFFu;
     const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
     uint32_t diag = diag_top, f = f_top, tx = T.x, ty = T.y;
 #pragma unroll
@@ -237,8 +248,7 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
         const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
         const uint32_t En = pk_max3(toe, em, NN);
         const uint32_t Fn = pk_max3(toe, fm, NN);
-        const uint32_t HC = H + C, toeC = toe + C;
-        const uint32_t fu = HC - tmp, fw = HC - f, fx = toeC - em, fy = toeC - fm;
+        const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, em), fy = tb_flag(toe, fm);
         // bytes: [u, x] per half and [w, y] per half, 0x00 / 0xFF
         const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
         const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
@@ -269,7 +279,6 @@ __device__ __forceinline__ void step_local_tb(const uint2 T, const int32_t c, co
                                               uint32_t (&dw)[R], uint32_t &f_out, const uint32_t KK,
                                               const uint32_t OEK, const uint32_t EXT, const uint32_t BB,
                                               const uint32_t KMUL, const uint32_t bshift, const int j) {
-    constexpr uint32_t C = 0x7FFF7FFFu;
     const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
     const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
     const uint32_t invc = ((col - bshift) & 0xFFFFu) * 0x10001u;   // key = H*256 + col (mod 2^16)
@@ -285,8 +294,7 @@ __device__ __forceinline__ void step_local_tb(const uint2 T, const int32_t c, co
         const uint32_t En = pk_max3(toe, em, BB);
         const uint32_t Fn = pk_max3(toe, fm, BB);
         key[k] = pk_max_u16(key[k], pk_mad_u16(H, KMUL, invc));
-        const uint32_t HC = H + C, toeC = toe + C;
-        const uint32_t fu = HC - tmp, fw = HC - f, fx = toeC - em, fy = toeC - fm;
+        const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, em), fy = tb_flag(toe, fm);
         const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
         const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
         dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
