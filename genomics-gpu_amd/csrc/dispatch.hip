@@ -181,6 +181,12 @@ static bool int16_safe(const gasalx_params &p, uint32_t mq, uint32_t mt) {
     return std::abs((int64_t)p.gap_open) + L * step < 30000;
 }
 
+// A/B switch: the environment variable, read as an integer, or `dflt` when unset
+static bool env_flag(const char *name, bool dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) != 0 : dflt;
+}
+
 // Packed banded kernel (banded16.hpp): stored values B + [0, Hmax] and keys
 // H*8 + 7 + 0x400 inside [0x0400, 0x7BFF]; pads score -b, which needs an N score
 // <= 0.  GASALX_BAND16=0 keeps every pair on the int32 kernel (A/B runs).
@@ -711,7 +717,8 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
     int32_t *qend = out.q_end, *tend = out.t_end;
     const bool wf_start = pl.kind == PLAN_WAVEFRONT && (p.algo == 3 || p.algo == 2) && p.start_pos == 1 &&
                           (out.q_start || out.t_start);
-    if (runs_tb) HIPCHK(ws.tb.reserve((size_t)n * tb_words * 4 + 64));
+    // (whole groups of 8 pairs: the packed kernels' interleaved layout, tb_store_window)
+    if (runs_tb) HIPCHK(ws.tb.reserve((size_t)((n + 7) & ~7u) * tb_words * 4 + 64));
     if (runs_tb || wf_start) {
         if ((p.algo == 3 || p.algo == 2) && (!qend || !tend)) {
             HIPCHK(ws.ends_q.reserve((size_t)n * 4));
@@ -722,6 +729,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
     }
 
     const uint32_t *slot_of = nullptr;   // pair -> slot when the wavefront launch ran sorted
+    uint32_t tb_q8 = 0;                  // the packed TB kernels' interleaved layout
     if (pl.kind == PLAN_WAVEFRONT) {
         WfArgs A;
         std::memset(&A, 0, sizeof(A));
@@ -756,6 +764,10 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                 slot_of = inv;
             }
         }
+        // unsorted waves hold consecutive pairs: interleave their direction chunks
+        // (GASALX_TB_Q8=0: per-pair layout, A/B)
+        A.tb_q8 = (pl.packed16 && pl.tb && !A.perm && env_flag("GASALX_TB_Q8", true)) ? 1u : 0u;
+        tb_q8 = A.tb_q8;
         int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start && dp) {
@@ -907,7 +919,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         T.a = p.match; T.b = p.mismatch; T.o = p.gap_open; T.e = p.gap_extend;
         T.is_local = p.algo == 3;
         T.pk_flags = nullptr;
-        T.pk_ppb = 1; T.pk_R = 1; T.pk_G = 1; T.pk_rmagic = 0;
+        T.pk_ppb = 1; T.pk_R = 1; T.pk_G = 1; T.pk_rmagic = 0; T.pk_q8 = 0;
         T.pk_fix = nullptr;
         T.slot_of = slot_of;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
@@ -921,6 +933,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.pk_G = pl.G16;
             T.pk_rmagic = (uint32_t)((0x100000000ull + pl.R16 - 1) / pl.R16);
             T.pk_fix = ws.aux.as<int32_t>();
+            T.pk_q8 = tb_q8;
         }
         tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
         HIPCHK(hipGetLastError());

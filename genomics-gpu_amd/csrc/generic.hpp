@@ -576,6 +576,7 @@ struct TbArgs {
     // skewed uint16 layout: flag per block of pk_ppb pairs, R rows per lane
     const uint8_t *pk_flags;
     uint32_t pk_ppb, pk_R, pk_G, pk_rmagic;   // pk_rmagic = ceil(2^32 / pk_R)
+    uint32_t pk_q8;                     // packed chunks of 8 consecutive pairs interleaved (wavefront16.hpp tb_store_window)
     const int32_t *pk_fix;              // H' at the start cell (row ql, column tl) when both are pads
     const uint32_t *slot_of;            // pair -> slot of the DP launch when it ran sorted, or NULL
     int32_t sc_nn;                      // substitution score N vs N (GLOBAL rule)
@@ -612,7 +613,10 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
     else { i = (int)tl; j = (int)ql; }
     const bool pk = A.pk_flags && A.pk_flags[(A.slot_of ? A.slot_of[tid] : tid) / A.pk_ppb];
-    const uint16_t *tb16 = reinterpret_cast<const uint16_t *>(tb);
+    // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
+    // pair at 8 * c + (tid & 7)
+    const bool il8 = pk && A.pk_q8;
+    const uint16_t *tb16 = reinterpret_cast<const uint16_t *>(il8 ? A.tb + (uint64_t)(tid & ~7u) * A.tb_pair_words : tb);
     // packed kernel: the start cell (ql, tl), both pads, was scored with the pad
     // row's -K instead of N==N.  Its E and F are exact, so with H' the value it
     // did compute, the true cell takes the diagonal iff score + sc(N,N) >= H'.
@@ -649,7 +653,8 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 // one 8-byte chunk (4 rows x 4 steps) per miss: the walk is bound by the
                 // lines it fetches (a 2 x 2 block of chunks per miss fetched 1.6x the lines
                 // and took 1.19 ms instead of 0.70, profiles/r03_tb_walk.md)
-                const int64_t key = (int64_t)(s >> 2) * (A.pk_G * A.pk_R) + ((k >> 2) * A.pk_G + lane) * 4;
+                const int64_t key = il8 ? (((int64_t)(s >> 2) * (A.pk_R >> 2) + (k >> 2)) * A.pk_G + lane) * 32 + (tid & 7u) * 4
+                                       : (int64_t)(s >> 2) * (A.pk_G * A.pk_R) + ((k >> 2) * A.pk_G + lane) * 4;
                 if (key != chunk_key) {
                     const uint2 c2 = *reinterpret_cast<const uint2 *>(tb16 + key);
                     chunk = make_uint4(c2.x, c2.y, 0u, 0u);

@@ -336,6 +336,50 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
 }
 
 // ---------------------------------------------------------------------------
+// Direction-flag stores of the packed traceback kernels, one 4-step window w.
+// A chunk is 4 rows x 4 steps of one pair (8 bytes, rows k..k+3 of lane lg).
+//  * per pair (tb_q8 = 0; sorted launches): window w of a pair holds G*R uint16,
+//    row lg*R + k at ((k/4)*G + lg)*4 + k%4, so a lane group's store is 8*G
+//    contiguous bytes;
+//  * interleaved (tb_q8 = 1; unsorted launches, whose waves hold 8 consecutive
+//    pairs): the 8 pairs of a wave share one region at pair (p & ~7), chunk
+//    ((w*R/4 + k/4)*G + lg)*8 + (p & 7).  A lane's two halves are adjacent pairs,
+//    so it stores both chunks as one 16-byte word and a wave's store is 1 KB
+//    contiguous; walks of neighbouring pairs that sit at the same cell read the
+//    same line (tb_kernel, profiles/r03_tb_walk.md).
+// ---------------------------------------------------------------------------
+template <int G, int R>
+__device__ __forceinline__ void tb_store_window(const WfArgs &A, const uint32_t (&pr)[2], const bool (&valid)[2],
+                                                const uint32_t (&W16)[2], const uint32_t w, const uint32_t lg,
+                                                const uint32_t (&dw)[R]) {
+    if (A.tb_q8) {
+        if ((valid[0] && w < W16[0]) || (valid[1] && w < W16[1])) {
+            uint4 *dst = reinterpret_cast<uint4 *>(A.tb + (uint64_t)(pr[0] & ~7u) * A.tb_pair_words) +
+                         ((uint64_t)w * (R / 4) * G + lg) * 4 + ((pr[0] & 7u) >> 1);
+#pragma unroll
+            for (int k = 0; k < R; k += 4)
+                dst[(k / 4) * G * 4] = make_uint4(__builtin_amdgcn_perm(dw[k + 1], dw[k], 0x05040100u),
+                                                  __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x05040100u),
+                                                  __builtin_amdgcn_perm(dw[k + 1], dw[k], 0x07060302u),
+                                                  __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x07060302u));
+        }
+        return;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (valid[h] && w < W16[h]) {
+            uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
+                            (uint64_t)w * (G * R) + lg * 4;
+            const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+#pragma unroll
+            for (int k = 0; k < R; k += 4)
+                *reinterpret_cast<uint2 *>(dst + k * G) =
+                    make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel), __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // The kernel.
 // ---------------------------------------------------------------------------
 constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront16 only)
@@ -524,21 +568,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 qstep(1, HB, HA);
                 qstep(2, HA, HB);
                 qstep(3, HB, HA);
-                const uint32_t w = s >> 2;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (valid[h] && w < W16[h]) {
-                        // lane-contiguous windows, as the GLOBAL+TB kernel's
-                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                        (uint64_t)w * (G * R) + lg * 4;
-                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
-#pragma unroll
-                        for (int k = 0; k < R; k += 4)
-                            *reinterpret_cast<uint2 *>(dst + k * G) =
-                                make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
-                                           __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
-                    }
-                }
+                tb_store_window<G, R>(A, pr, valid, W16, s >> 2, lg, dw);   // layout: see tb_store_window
             }
         } else {
             uint32_t s = 0;
@@ -707,11 +737,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             recvF = (uint32_t)shr_lane((int32_t)f);
         };
         if constexpr (GTB) {
-            // Direction flags, skewed layout (read by tb_kernel): per pair, windows
-            // w = (column + lane) / 4 of G*R uint16 holding the 4-step window's flags,
-            // row lane*R + k at ((k/4)*G + lane)*4 + k%4 — every lane stores after the
-            // same steps, and the G lanes of a group write 8*G contiguous bytes per
-            // store (-5 % kernel time against [w][row], r02_tb_store_ab.md).
+            // Direction flags, skewed layout (read by tb_kernel): windows w = (column +
+            // lane) / 4 holding the 4-step window's flags, every lane stores after the
+            // same steps (tb_store_window: per pair, or 8 pairs interleaved).
             static_assert(R % 4 == 0, "GLOBAL+TB packed shapes need R % 4 == 0");
             uint32_t W16[2];
 #pragma unroll
@@ -762,21 +790,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     }
                 }
 #else
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (valid[h] && w < W16[h]) {
-                        // window w of a pair: G*R uint16, row lg*R + k at ((k/4)*G + lg)*4 + k%4,
-                        // so a lane group's store is 8*G contiguous bytes
-                        uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                        (uint64_t)w * (G * R) + lg * 4;
-                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
-#pragma unroll
-                        for (int k = 0; k < R; k += 4)
-                            *reinterpret_cast<uint2 *>(dst + k * G) =
-                                make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
-                                           __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
-                    }
-                }
+                tb_store_window<G, R>(A, pr, valid, W16, w, lg, dw);   // layout: see tb_store_window
 #endif
             }
 #if GX_WF16_CAPTURE_TREE
