@@ -81,6 +81,11 @@ WORKLOADS = {
                         label="second front-end (nvbio BatchedAlignmentScore idiom, sw-benchmark.cu:585-615): "
                               "Gotoh (2,-1,-2,-1) semi-global, 256K 150bp reads (4-bit DNA_N) per GPU against one "
                               "1,000bp 2-bit reference, seed 0x5EED0006"),
+    "nvbio_banded": dict(kind=6, band=16, pairs=1_048_576, scaling="weak", params=None, bytes=128, ops=9,
+                         label="second front-end, banded (nvbio BatchedBandedAlignmentScore<16>, batched.h:337): "
+                               "Gotoh (2,-1,-2,-1) semi-global, 1M 150bp reads (4-bit DNA_N) per GPU, each against "
+                               "its 165bp reference window (2-bit) starting 7bp before the read's origin; cells = "
+                               "the band's (150 x 16 per pair), seed 0x5EED0006"),
     "cpu_plumbing": dict(kind=1, pairs=1024, scaling="weak", params=dict(algo=G.LOCAL), bytes=152, ops=12,
                          label="config1: 1024 pairs 64x64 SW local through the host-side CPU verify scorer "
                                "(oracle/), same batch through the GPU, seed 0x5EED0001"),
@@ -88,6 +93,7 @@ WORKLOADS = {
 METRICS = {
     "pairhmm": "GCUPS of PairHMM fp32 forward (config 5, 250x500) on MI355X",
     "nvbio_gotoh": "GCUPS of nvbio-style batched Gotoh semi-global scoring (sw-benchmark idiom) on MI355X",
+    "nvbio_banded": "GCUPS (band cells) of nvbio-style banded (16) Gotoh semi-global scoring on MI355X",
     "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
 }
 SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006}
@@ -184,7 +190,7 @@ def pack_uniform(codes, bits, big):
     return np.bitwise_or.reduce(flat.reshape(-1, per) << shift, axis=1).astype(np.uint32)
 
 
-def synth_nvbio(start, n, seed):
+def synth_nvbio(start, n, seed, band=0):
     """Reads of 150 bp taken from a 1,000 bp random reference at uniform offsets with
     5% substitutions (N included, as DNA_N reads carry them); blocks of 8,192 reads
     from default_rng((seed, block)) so a rank generates only its shard.  Codes:
@@ -203,7 +209,32 @@ def synth_nvbio(start, n, seed):
     codes = np.concatenate(reads).reshape(-1)
     pat = G.PackedSet(pack_uniform(codes, 4, True), np.arange(n + 1, dtype=np.uint32) * NV_READ_LEN, 0, 4, True)
     txt = G.PackedSet(pack_uniform(ref, 2, False), None, NV_REF_LEN, 2, False)
+    if band:
+        # banded: each read against its own window of NV_READ_LEN + band - 1 symbols that
+        # starts band // 2 before the read's origin (clamped to the reference)
+        wl_ = NV_READ_LEN + band - 1
+        sts = []
+        for b in range(b0, b1):
+            st = np.random.default_rng((seed, b)).integers(0, NV_REF_LEN - NV_READ_LEN + 1, PH_BLOCK)
+            lo, hi = max(start, b * PH_BLOCK) - b * PH_BLOCK, min(start + n, (b + 1) * PH_BLOCK) - b * PH_BLOCK
+            sts.append(st[lo:hi])
+        w0 = np.clip(np.concatenate(sts) - band // 2, 0, NV_REF_LEN - wl_)
+        tcodes = ref[w0[:, None] + np.arange(wl_)[None, :]].reshape(-1)
+        txt = G.PackedSet(pack_uniform(tcodes, 2, False), np.arange(n + 1, dtype=np.uint32) * wl_, 0, 2, False)
+        return dict(codes=codes, pat=pat, txt=txt, band=band, tcodes=tcodes, wlen=wl_)
     return dict(codes=codes, pat=pat, txt=txt)
+
+
+def nv_oracle(O, nv, sub, n_threads, lo=0, hi=None):
+    """The oracle over reads [lo, hi) of a kind-6 batch (sub: their packed patterns)."""
+    al = G.NvAligner(**NV_ALIGNER)
+    if not nv.get("band"):
+        return O.nv_score(al, sub, nv["txt"], n_threads=n_threads)
+    w = nv["wlen"]
+    hi = len(nv["pat"].offsets) - 1 if hi is None else hi
+    t = G.PackedSet(pack_uniform(nv["tcodes"][lo * w:hi * w], 2, False), np.arange(hi - lo + 1, dtype=np.uint32) * w,
+                    0, 2, False)
+    return O.nv_banded_score(al, nv["band"], sub, t, n_threads=n_threads)
 
 
 def nv_subset(nv, e):
@@ -308,9 +339,9 @@ def single_core_rate(O, kind, data, pkw, budget_s):
             sub = G.PackedSet(pack_uniform(codes, 4, True), np.arange(e - done + 1, dtype=np.uint32) * NV_READ_LEN,
                               0, 4, True)
             t0 = time.perf_counter()
-            O.nv_score(G.NvAligner(**NV_ALIGNER), sub, data["txt"], n_threads=1)
+            nv_oracle(O, data, sub, 1, done, e)
             used += time.perf_counter() - t0
-            cells += (e - done) * NV_READ_LEN * NV_REF_LEN
+            cells += (e - done) * NV_READ_LEN * (data.get("band") or NV_REF_LEN)
         elif kind == 5:
             sub = {k: (v[done * 250:e * 250] if k in ("reads", "qm", "delta", "xiksi", "alpha")
                        else v[done * 500:e * 500] if k == "haps" else v[done:e]) for k, v in data.items()}
@@ -365,7 +396,10 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
     """PCIe-inclusive rate through the host-buffer entry point (gasalx_align_host /
     gasalx_pairhmm_host): host arrays in, H2D + kernels + D2H, results back in host
     arrays.  Reported beside `value`, never as it."""
-    if kind == 6:
+    if kind == 6 and data.get("band"):
+        call = lambda: eng.nv_banded_score_host(G.NvAligner(**NV_ALIGNER), data["band"], data["pat"], data["txt"])
+        path = "gasalx_nv_banded_score_host (pageable host arrays; H2D + kernel + D2H)"
+    elif kind == 6:
         call = lambda: eng.nv_score_host(G.NvAligner(**NV_ALIGNER), data["pat"], data["txt"])
         path = "gasalx_nv_score_host (pageable host arrays; H2D + kernel + D2H)"
     elif kind == 5:
@@ -554,20 +588,27 @@ def main():
                            backend=backend) if do_gather else None
     t_syn = time.perf_counter()
     if kind == 6:
-        nv = synth_nvbio(start, n, seed)
+        band = wl.get("band", 0)
+        nv = synth_nvbio(start, n, seed, band)
         data = nv
-        cells_per_step = n * rl * hl
+        cells_per_step = n * rl * (band or hl)
         al = G.NvAligner(**NV_ALIGNER)
         dpw = torch.from_numpy(nv["pat"].words.view(np.int32)).to(dev)
         dpo = torch.from_numpy(nv["pat"].offsets.view(np.int32)).to(dev)
         dtw = torch.from_numpy(nv["txt"].words.view(np.int32)).to(dev)
+        dto = torch.from_numpy(nv["txt"].offsets.view(np.int32)).to(dev) if band else None
         result = gather.buf if gather else torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         pat = {"words": dpw.data_ptr(), "offsets": dpo.data_ptr(), "bits": 4, "big_endian": True}
-        txt = {"words": dtw.data_ptr(), "offsets": 0, "length": NV_REF_LEN, "bits": 2, "big_endian": False}
-        plan = G.nv_describe_plan(al, rl, hl)
+        txt = {"words": dtw.data_ptr(), "offsets": dto.data_ptr() if band else 0, "length": 0 if band else NV_REF_LEN,
+               "bits": 2, "big_endian": False}
+        plan = f"nvbanded_gotoh_semi_B{band} (thread per pair, band in registers)" if band else \
+            G.nv_describe_plan(al, rl, hl)
 
         def align():
-            eng.nv_score_device_ptrs(al, n, pat, txt, result.data_ptr(), 0, rl, hl, stream.cuda_stream)
+            if band:
+                eng.nv_banded_score_device_ptrs(al, band, n, pat, txt, result.data_ptr(), stream.cuda_stream)
+            else:
+                eng.nv_score_device_ptrs(al, n, pat, txt, result.data_ptr(), 0, rl, hl, stream.cuda_stream)
 
         def results():
             return {"score": result[:n].cpu().numpy()}
@@ -678,7 +719,7 @@ def main():
         got = results()
         t_o = time.perf_counter()
         if kind == 6:
-            ref = O.nv_score(G.NvAligner(**NV_ALIGNER), nv_subset(data, m), data["txt"], n_threads=threads)
+            ref = nv_oracle(O, data, nv_subset(data, m), threads, 0, m)
             mism = {"score": int(np.count_nonzero(got["score"][:m] != ref))}
             extra = {}
             ref_scores = ref
@@ -699,7 +740,7 @@ def main():
             mism, extra = compare_align(gsub, ref, fields, batch=sub, cigar=tb)
             ref_scores = ref["score"]
         oracle_s = time.perf_counter() - t_o
-        cells_checked = (m * rl * hl)
+        cells_checked = m * rl * ((data.get("band") or hl) if kind == 6 else hl)
         tot = torch.tensor([m, sum(mism.values())], dtype=torch.int64, device=dev)
         gather_bad = 0
         if gather is not None:

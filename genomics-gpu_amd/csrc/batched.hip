@@ -11,6 +11,7 @@
 #include "engine.hpp"
 #include "nvbio.hpp"
 #include "nvbio16.hpp"
+#include "nvbanded.hpp"
 
 namespace gx {
 
@@ -197,6 +198,47 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
     set_error("pattern longer than 1024 or text too long for LDS (" + std::to_string(max_p) + ", " +
               std::to_string(max_t) + ")");
     return GASALX_ERANGE;
+}
+
+// ---- BatchedBandedAlignmentScore<band> (nvbanded.hpp): thread per pair, band in registers,
+//      instances for bands up to 8, 16 and 32 ----
+namespace {
+using NvBandFn = void (*)(NvBandArgs);
+template <int ALN, int TYPE>
+NvBandFn nv_band_pick(uint32_t band) {
+    if (band <= 8) return &nv_banded_kernel<ALN, TYPE, 8>;
+    if (band <= 16) return &nv_banded_kernel<ALN, TYPE, 16>;
+    if (band <= 32) return &nv_banded_kernel<ALN, TYPE, 32>;
+    return nullptr;
+}
+template <int ALN>
+NvBandFn nv_band_lookup_t(int type, uint32_t band) {
+    return type == NV_GLOBAL ? nv_band_pick<ALN, NV_GLOBAL>(band)
+         : type == NV_SEMI ? nv_band_pick<ALN, NV_SEMI>(band) : nv_band_pick<ALN, NV_LOCAL>(band);
+}
+}  // namespace
+
+int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
+                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st) {
+    if (al.aligner < 0 || al.aligner > 2 || al.type < 0 || al.type > 2) { set_error("bad aligner"); return GASALX_EINVAL; }
+    if (band < 2 || band > 32) { set_error("band length must be 2..32"); return GASALX_EINVAL; }
+    for (uint32_t b : {pat.bits, txt.bits})
+        if (b != 2 && b != 4 && b != 8) { set_error("symbol bits must be 2, 4 or 8"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    if (!pat.words || !pat.offsets || !txt.words || !scores) { set_error("null argument"); return GASALX_EINVAL; }
+    NvBandArgs A;
+    A.pw = pat.words; A.poff = pat.offsets; A.pbits = pat.bits; A.pbig = pat.big_endian;
+    A.tw = txt.words; A.toff = txt.offsets; A.tbits = txt.bits; A.tbig = txt.big_endian;
+    A.tlen0 = txt.offsets ? 0 : txt.length;
+    A.score = scores; A.n = n; A.band = band;
+    if (al.aligner == NV_ED) { A.match = 0; A.mismatch = -1; A.del = -1; A.ins = -1; }   // ed_banded_inl.h:63-78
+    else { A.match = al.match; A.mismatch = al.mismatch; A.del = al.deletion; A.ins = al.insertion; }
+    A.go = al.gap_open; A.ge = al.gap_ext;
+    NvBandFn fn = al.aligner == NV_GOTOH ? nv_band_lookup_t<NV_GOTOH>(al.type, band) : nv_band_lookup_t<NV_SW>(al.type, band);
+    hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+    return GASALX_OK;
 }
 
 }  // namespace gx

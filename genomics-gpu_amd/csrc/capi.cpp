@@ -593,6 +593,41 @@ int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32
     return GASALX_OK;
 }
 
+int gasalx_nv_banded_score_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
+                                  const gasalx_nv_strings *pat, const gasalx_nv_strings *txt, int32_t *scores,
+                                  void *stream) {
+    if (!eng || !al || !pat || !txt) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    CK(hipSetDevice(eng->device));
+    return gx::nv_banded_score_device(*al, band, n, *pat, *txt, scores, stream ? (hipStream_t)stream : eng->stream);
+}
+
+int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
+                                const gasalx_nv_strings *pat, uint64_t pat_words, const gasalx_nv_strings *txt,
+                                uint64_t txt_words, int32_t *scores) {
+    if (!eng || !al || !pat || !txt || !pat->words || !pat->offsets || !txt->words || !scores) {
+        gx::set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    if (band < 2 || band > 32) { gx::set_error("band length must be 2..32"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    gasalx_nv_strings dp = *pat, dt = *txt;
+    int rc;
+    uint32_t *p32;
+    if ((rc = stage_in(eng->nv_pw, pat->words, pat_words, st, &p32))) return rc; dp.words = p32;
+    if ((rc = stage_in(eng->nv_po, pat->offsets, (size_t)n + 1, st, &p32))) return rc; dp.offsets = p32;
+    if ((rc = stage_in(eng->nv_tw, txt->words, txt_words, st, &p32))) return rc; dt.words = p32;
+    if ((rc = stage_in(eng->nv_to, txt->offsets, txt->offsets ? (size_t)n + 1 : 0, st, &p32))) return rc;
+    dt.offsets = txt->offsets ? p32 : nullptr;
+    CK(eng->nv_s.reserve((size_t)n * 4));
+    rc = gx::nv_banded_score_device(*al, band, n, dp, dt, eng->nv_s.as<int32_t>(), st);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
 int gasalx_pairhmm_params(const uint8_t *bq, const uint8_t *iq, const uint8_t *dq, uint32_t n, float *qm,
                           float *delta, float *xiksi, float *alpha) {
     if (n && (!bq || !iq || !dq || !qm || !delta || !xiksi || !alpha)) return GASALX_EINVAL;

@@ -113,6 +113,9 @@ int pairhmm_quals_device(Workspace &ws, const gasalx_hmm_qual_batch &b, float *r
 int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
                     const gasalx_nv_strings &txt, int32_t *scores, int16_t *scores16, uint32_t max_p, uint32_t max_t,
                     hipStream_t stream);
+// nvbio BatchedBandedAlignmentScore<band> (batched.hip / nvbanded.hpp): BestSink score per pair
+int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
+                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st);
 std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text,
                          uint32_t text_bits);
 

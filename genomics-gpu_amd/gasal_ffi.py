@@ -33,6 +33,7 @@ EXPORTS = (
     "gasalx_synth_spec", "gasalx_synth_pairs", "gasalx_synth_range", "gasalx_host_alloc", "gasalx_host_free",
     "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
     "gasalx_nv_score_device", "gasalx_nv_score_host", "gasalx_nv_describe_plan",
+    "gasalx_nv_banded_score_device", "gasalx_nv_banded_score_host",
     "gasalx_multi_create", "gasalx_multi_destroy", "gasalx_multi_info", "gasalx_multi_engine",
     "gasalx_shard_bounds", "gasalx_multi_align_host", "gasalx_multi_pairhmm_host",
     "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather",
@@ -356,6 +357,29 @@ class Engine:
                                           ctypes.byref(texts.cstruct()), ctypes.c_uint64(len(texts.words)), _p(sc),
                                           _p(s16)), "nv_score_host")
         return (sc, s16) if int16 else sc
+
+    def nv_banded_score_host(self, aligner: "NvAligner", band: int, patterns: "PackedSet", texts: "PackedSet"):
+        """nvbio BatchedBandedAlignmentScore<band> (gasalx_nv_banded_score_host): BestSink
+        score per pair, INT32_MIN where a text is shorter than its pattern."""
+        n = patterns.n
+        sc = np.zeros(n, np.int32)
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_banded_score_host(self._h, ctypes.byref(ca), ctypes.c_uint32(band), ctypes.c_uint32(n),
+                                                 ctypes.byref(patterns.cstruct()),
+                                                 ctypes.c_uint64(len(patterns.words)), ctypes.byref(texts.cstruct()),
+                                                 ctypes.c_uint64(len(texts.words)), _p(sc)), "nv_banded_score_host")
+        return sc
+
+    def nv_banded_score_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
+                                    scores_ptr: int, stream: int = 0):
+        """Device-resident banded scoring (gasalx_nv_banded_score_device); pat/txt as nv_score_device_ptrs."""
+        mk = lambda d: CNvStrings(d["words"], d.get("offsets") or None, d.get("length", 0), d["bits"],
+                                  int(d.get("big_endian", False)))
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_banded_score_device(self._h, ctypes.byref(ca), ctypes.c_uint32(band), ctypes.c_uint32(n),
+                                                   ctypes.byref(mk(pat)), ctypes.byref(mk(txt)),
+                                                   ctypes.c_void_p(scores_ptr or None), ctypes.c_void_p(stream or None)),
+               "nv_banded_score_device")
 
     def nv_score_device_ptrs(self, aligner: "NvAligner", n: int, pat: dict, txt: dict, scores_ptr: int = 0,
                              scores16_ptr: int = 0, max_pattern_len: int = 0, max_text_len: int = 0, stream: int = 0):

@@ -257,6 +257,18 @@ int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, u
                          const gasalx_nv_strings *patterns, uint64_t pattern_words, const gasalx_nv_strings *texts,
                          uint64_t text_words, int32_t *scores, int16_t *scores16);
 
+/* nvbio's BatchedBandedAlignmentScore<band_len> (NvB/nvbio/alignment/batched.h:337,
+ * batched_banded_inl.h:44-75): the banded DP of sw_banded_inl.h / gotoh_banded_inl.h /
+ * ed_banded_inl.h over cells (i, i + j), 0 <= j < band_len (2..32), one pair per thread.
+ * BestSink score per pair; INT32_MIN when a text is shorter than its pattern (skipped,
+ * as the reference does). */
+int gasalx_nv_banded_score_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band_len,
+                                  uint32_t n_pairs, const gasalx_nv_strings *dev_patterns,
+                                  const gasalx_nv_strings *dev_texts, int32_t *dev_scores, void *stream);
+int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band_len,
+                                uint32_t n_pairs, const gasalx_nv_strings *patterns, uint64_t pattern_words,
+                                const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores);
+
 /* Multi-GPU from one host process.  A group holds one engine per
  * entry of a device list (entries may repeat a device); a host batch is split into
  * contiguous ranges of pairs with equal cell counts (Σ ql·tl; gasalx_shard_bounds),

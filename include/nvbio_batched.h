@@ -7,12 +7,15 @@
  *   the scheduler tags                                      batched.h:44-87
  *   SimpleSmithWatermanScheme / SimpleGotohScheme           alignment/utils.h:92-135
  *   make_{edit_distance,smith_waterman,gotoh}_aligner       alignment/alignment_base.h:180-330
+ *   nvbio::aln::BatchedBandedAlignmentScore<BAND_LEN, stream, scheduler>
+ *                                                           batched.h:337-352, batched_banded_inl.h:44-75
  *   sw-benchmark's AlignmentStream (reads 4-bit DNA_N big-endian, reference 2-bit,
  *   int16 scores)                                           NvB/sw-benchmark/sw-benchmark.cu:100-215
  * Every scheduler maps to the same MI355X kernel (nvbio.hpp: lane groups per pattern,
- * text in LDS); there is no temporary storage, so max_temp_storage() is 0.  Only the
- * TextBlockingTag / PatternBlockingTag score semantics are provided (both give the same
- * scores); traceback, banded and warp variants of nvbio are not.
+ * text in LDS; banded: nvbanded.hpp, one pair per thread with the band in registers);
+ * there is no temporary storage, so max_temp_storage() is 0.  The TextBlockingTag /
+ * PatternBlockingTag score semantics are provided (both give the same scores), full and
+ * banded; nvbio's traceback and warp variants are not.
  *
  * Header-only C++ over the flat C-ABI (gasalx.h); link with -lgasal.
  */
@@ -198,6 +201,38 @@ struct BatchedAlignmentScore {
                                               stream.max_text_length(), hip_stream);
         if (rc != GASALX_OK) {
             fprintf(stderr, "BatchedAlignmentScore::enact: %s\n", gasalx_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
+};
+
+// Banded scoring (batched_banded_inl.h:44-75): every pattern against the first
+// pattern_length + BAND_LEN - 1 symbols of its text, cells (i, i + j) with j < BAND_LEN
+// (2..32).  Scores are int32 (stream.m_scores32); a text shorter than its pattern is
+// skipped and scores INT32_MIN, as nvbio's BestSink leaves it.
+template <uint32 BAND_LEN, typename stream_type, typename scheduler_type = DeviceThreadScheduler>
+struct BatchedBandedAlignmentScore {
+    typedef stream_type input_stream_type;
+    typedef typename stream_type::aligner_type aligner_type;
+
+    static uint64 min_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+    static uint64 max_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+
+    void enact(stream_type stream, uint64 temp_size = 0u, uint8 *temp = NULL, void *hip_stream = NULL) {
+        (void)temp_size; (void)temp;
+        const gasalx_nv_aligner a = stream.aligner().c_aligner();
+        gasalx_nv_strings p = {stream.m_patterns, stream.m_offsets, 0, stream.m_pattern_bits,
+                               stream.m_pattern_big_endian};
+        gasalx_nv_strings t = {stream.m_text, stream.m_text_offsets, stream.m_text_len, stream.m_text_bits,
+                               stream.m_text_big_endian};
+        if (stream.m_scores32 == NULL) {
+            fprintf(stderr, "BatchedBandedAlignmentScore::enact: banded scores are int32, set m_scores32\n");
+            exit(EXIT_FAILURE);
+        }
+        const int rc = gasalx_nv_banded_score_device(engine(), &a, BAND_LEN, stream.size(), &p, &t,
+                                                     stream.m_scores32, hip_stream);
+        if (rc != GASALX_OK) {
+            fprintf(stderr, "BatchedBandedAlignmentScore::enact: %s\n", gasalx_last_error());
             exit(EXIT_FAILURE);
         }
     }

@@ -99,6 +99,14 @@ int orc_nv_score_batch(int aligner, int type, const int32_t prm[6], uint32_t n,
                        const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
                        const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
                        int32_t *scores, int n_threads);
+/* nvbio banded score (BatchedBandedAlignmentScore<band>): same arguments plus the band
+ * length (>= 2); BestSink score per pair, INT32_MIN when text_len < pattern_len. */
+int32_t orc_nv_banded_score_one(int aligner, int type, const int32_t prm[6], uint32_t band, const uint32_t *pat,
+                                uint32_t M, const uint32_t *txt, uint32_t N);
+int orc_nv_banded_score_batch(int aligner, int type, const int32_t prm[6], uint32_t band, uint32_t n,
+                              const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                              const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
+                              int32_t *scores, int n_threads);
 
 #ifdef __cplusplus
 }

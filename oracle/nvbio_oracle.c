@@ -17,8 +17,20 @@
  *   utils.h:92-135               SimpleSmithWatermanScheme / SimpleGotohScheme
  * The infimum is Field_traits<int32>::min() - min(Go, Ge) (gotoh_inl.h:1162), int32 columns.
  *
- * Parity status: nvbio needs CUDA + thrust to build, so this restatement is pinned only by
- * hand-derived known answers (tests/test_nvbio_oracle.py) — "parity unpinned" otherwise.
+ * Banded (orc_nv_banded_*; NvB/nvbio/alignment/batched_banded_inl.h:44-75 per pair):
+ *   sw/sw_banded_inl.h:44-54      row zero: band[j] = GLOBAL ? j * deletion : 0
+ *   sw/sw_banded_inl.h:361-512    rows: band[j] = H(i, i + j); j = 0 has no left, j = B-1 no top;
+ *                                 top = band[j+1] + deletion, left = band[j-1] + insertion;
+ *                                 sinks: LOCAL every cell, GLOBAL band[B-1], SEMI band[j < m]
+ *   gotoh/gotoh_banded_inl.h:44-75, 405-666  the same with F (vertical, per band slot) and E
+ *                                 (horizontal, carried along the row); F[B-1] = infimum
+ *   ed/ed_banded_inl.h:63-78      edit distance = the SW form with (0, -1, -1, -1)
+ *   the alignment is skipped (BestSink stays INT32_MIN) when text_len < pattern_len.
+ *
+ * Parity status: nvbio needs CUDA + thrust to build.  The restatement is pinned by the
+ * reference's own unit-test vectors (NvB/nvbio-test/alignment_test.cu:680-793 via
+ * tests/golden/nvbio_reference_kats.json: CIGAR-implied optima and the banded edit-distance
+ * cases) and by hand-derived known answers (tests/test_nvbio_oracle.py).
  */
 #include <limits.h>
 #include <stdint.h>
@@ -118,6 +130,117 @@ int orc_nv_score_batch(int aligner, int type, const int32_t prm[6], uint32_t n,
         for (uint32_t i = 0; i < M; i++) p[i] = nv_sym(pw, pbits, pbig, (uint64_t)poff[k] + i);
         for (uint32_t i = 0; i < N; i++) t[i] = nv_sym(tw, tbits, tbig, t0 + i);
         scores[k] = orc_nv_score_one(aligner, type, prm, p, M, t, N);
+        free(p);
+        free(t);
+    }
+    return 0;
+}
+
+/*
+ * Banded score, one pair (see the header for the reference lines).  Text symbols are
+ * read as 255 past text_len: the row loop's guard (sw_banded_inl.h:453,
+ * gotoh_banded_inl.h:597); the reference's first-band load (:375 / :433) has no guard
+ * and reads past the string only when text_len < band - 1.
+ */
+int32_t orc_nv_banded_score_one(int aligner, int type, const int32_t prm[6], uint32_t band, const uint32_t *pat,
+                                uint32_t M, const uint32_t *txt, uint32_t N) {
+    int32_t match = prm[0], mismatch = prm[1], Go = prm[2], Ge = prm[3], Del = prm[4], Ins = prm[5];
+    if (aligner == ORC_NV_ED) { match = 0; mismatch = -1; Del = -1; Ins = -1; }
+    int32_t best = INT32_MIN;                                  /* BestSink() */
+    if (N < M || band < 2) return best;
+    const uint32_t B = band;
+    int32_t *H = (int32_t *)malloc(B * sizeof(int32_t)), *F = (int32_t *)malloc(B * sizeof(int32_t));
+    /* gotoh_banded_inl.h:440-442: Field_traits<short>::min() - max(Go, Ge, text Go, text Ge) */
+    const int32_t infimum = -32768 - (Go > Ge ? Go : Ge);
+#define TXT(k) ((k) < N ? txt[k] : 255u)
+    if (aligner == ORC_NV_GOTOH) {
+        H[0] = 0;
+        for (uint32_t j = 1; j < B; j++) H[j] = type == ORC_NV_GLOBAL ? Go + (int32_t)(j - 1) * Ge : 0;
+        for (uint32_t j = 0; j < B; j++) F[j] = infimum;
+        for (uint32_t i = 0; i < M; i++) {
+            const uint32_t q = pat[i];
+            int32_t hi;
+            {   /* j == 0 */
+                F[0] = nmax(F[1] + Ge, H[1] + Go);
+                const int32_t diag = H[0] + (TXT(i) == q ? match : mismatch);
+                hi = nmax(F[0], diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[0] = hi;
+            }
+            int32_t E = H[0] + Go;
+            for (uint32_t j = 1; j + 1 < B; j++) {
+                F[j] = nmax(F[j + 1] + Ge, H[j + 1] + Go);
+                const int32_t diag = H[j] + (TXT(i + j) == q ? match : mismatch);
+                hi = nmax(nmax(F[j], E), diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[j] = hi;
+                E = nmax(hi + Go, E + Ge);
+            }
+            {   /* j == B-1 */
+                F[B - 1] = infimum;
+                const int32_t diag = H[B - 1] + (TXT(i + B - 1) == q ? match : mismatch);
+                hi = nmax(E, diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[B - 1] = hi;
+            }
+        }
+    } else {
+        for (uint32_t j = 0; j < B; j++) H[j] = type == ORC_NV_GLOBAL ? (int32_t)j * Del : 0;
+        for (uint32_t i = 0; i < M; i++) {
+            const uint32_t q = pat[i];
+            int32_t hi;
+            {   /* j == 0: top and diagonal */
+                const int32_t diag = H[0] + (TXT(i) == q ? match : mismatch);
+                hi = nmax(H[1] + Del, diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[0] = hi;
+            }
+            for (uint32_t j = 1; j + 1 < B; j++) {
+                const int32_t diag = H[j] + (TXT(i + j) == q ? match : mismatch);
+                hi = nmax(nmax(H[j + 1] + Del, H[j - 1] + Ins), diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[j] = hi;
+            }
+            {   /* j == B-1: left and diagonal */
+                const int32_t diag = H[B - 1] + (TXT(i + B - 1) == q ? match : mismatch);
+                hi = nmax(H[B - 2] + Ins, diag);
+                if (type == ORC_NV_LOCAL) { hi = nmax(hi, 0); if (best <= hi) best = hi; }
+                H[B - 1] = hi;
+            }
+        }
+    }
+#undef TXT
+    if (type == ORC_NV_GLOBAL) {
+        if (best <= H[B - 1]) best = H[B - 1];
+    } else if (type == ORC_NV_SEMI_GLOBAL) {
+        const uint32_t m = (M + B - 1 < N ? M + B - 1 : N) - (M - 1);
+        if (best <= H[0]) best = H[0];
+        for (uint32_t j = 1; j < B; j++)
+            if (j < m && best <= H[j]) best = H[j];
+    }
+    free(H);
+    free(F);
+    return best;
+}
+
+int orc_nv_banded_score_batch(int aligner, int type, const int32_t prm[6], uint32_t band, uint32_t n,
+                              const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                              const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
+                              int32_t *scores, int n_threads) {
+    if (!prm || !pw || !poff || !tw || !scores || band < 2) return -1;
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads)
+#endif
+    for (long k = 0; k < (long)n; k++) {
+        const uint32_t M = poff[k + 1] - poff[k];
+        const uint64_t t0 = toff ? toff[k] : 0;
+        const uint32_t N = toff ? toff[k + 1] - toff[k] : tlen0;
+        uint32_t *p = (uint32_t *)malloc((M + 1) * sizeof(uint32_t));
+        uint32_t *t = (uint32_t *)malloc((N + 1) * sizeof(uint32_t));
+        for (uint32_t i = 0; i < M; i++) p[i] = nv_sym(pw, pbits, pbig, (uint64_t)poff[k] + i);
+        for (uint32_t i = 0; i < N; i++) t[i] = nv_sym(tw, tbits, tbig, t0 + i);
+        scores[k] = orc_nv_banded_score_one(aligner, type, prm, band, p, M, t, N);
         free(p);
         free(t);
     }

@@ -156,3 +156,20 @@ def nv_score(aligner, patterns, texts, n_threads=0):
         raise RuntimeError(f"orc_nv_score_batch failed ({rc})")
     return out
 
+
+
+def nv_banded_score(aligner, band, patterns, texts, n_threads=0):
+    """nvbio banded score restatement (nvbio_oracle.c orc_nv_banded_*): BatchedBandedAlignmentScore<band>."""
+    n = len(patterns.offsets) - 1
+    out = np.zeros(n, np.int32)
+    lib().orc_nv_banded_score_batch.restype = ctypes.c_int
+    rc = lib().orc_nv_banded_score_batch(ctypes.c_int(aligner.aligner), ctypes.c_int(aligner.type),
+                                         _ptr(aligner.prm()), ctypes.c_uint32(band), ctypes.c_uint32(n),
+                                         _ptr(patterns.words), _ptr(patterns.offsets), ctypes.c_uint32(patterns.bits),
+                                         ctypes.c_uint32(int(patterns.big_endian)), _ptr(texts.words),
+                                         _ptr(texts.offsets), ctypes.c_uint32(texts.length),
+                                         ctypes.c_uint32(texts.bits), ctypes.c_uint32(int(texts.big_endian)),
+                                         _ptr(out), ctypes.c_int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"orc_nv_banded_score_batch failed ({rc})")
+    return out

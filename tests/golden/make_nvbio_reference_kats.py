@@ -11,6 +11,10 @@ nvbio unit test holds (NvB/nvbio-test/alignment_test.cu), restated as scores.
   backwards (:654-658).  The optimum each CIGAR implies is therefore the best score of the
   reversed op string over its placements in the text (the traceback's placement is one of
   them and is optimal; no placement can beat the optimum).
+* :790 runs the banded (band 7) Gotoh SEMI_GLOBAL case of the same strings and asserts the
+  banded traceback's CIGAR 4M1D3M and that its score equals ref_banded_sw's (:296-356): the
+  banded optimum is the best score of that op string over the placements whose cells all
+  lie inside the band (cell (i, c) in the band when 0 <= c - i < 7).
 * :680-745 holds banded (band 5) SEMI_GLOBAL edit-distance cases with stated scores.
   They are kept with the band; the test asserts them against the full-DP front-end where
   the full DP computes the same value (every case here: each optimum lies inside the band).
@@ -94,6 +98,35 @@ def implied(cigar, kind, type_):
     return best
 
 
+def in_band_placements(ops, band):
+    """Text starts whose path keeps every cell (i, c) at 0 <= c - i < band (leading text gaps
+    are the free semi-global start and carry no cell)."""
+    out = []
+    for st in range(band):
+        i, k, ok = 0, st, True
+        for op in ops:
+            if op == "M":
+                cell = k - i; i += 1; k += 1
+            elif op == "D":
+                cell = k - (i - 1) if i > 0 else 0; k += 1
+            else:
+                cell = k - 1 - i; i += 1
+            ok &= 0 <= cell < band
+        if ok:
+            out.append(st)
+    return out
+
+
+def implied_banded(cigar, kind, band):
+    ops = ops_of(cigar)[::-1]
+    best = None
+    for st in in_band_placements(ops, band):
+        sc = cigar_score(ops, PATTERN, TEXT, st, kind, SCHEMES[kind])
+        if sc is not None:
+            best = sc if best is None or sc > best else best
+    return best
+
+
 def main():
     cases = []
     for kind in ("sw", "gotoh"):
@@ -103,8 +136,11 @@ def main():
                               source="NvB/nvbio-test/alignment_test.cu:749-793"))
     ed = [dict(test_id=i, pattern=p, text=t, score=e, band=5, type="SEMI_GLOBAL",
                source="NvB/nvbio-test/alignment_test.cu:680-745") for i, p, t, e in ED_CASES]
-    json.dump({"alignment": cases, "edit_distance": ed}, open(OUT, "w"), indent=1)
-    print(OUT, [(c["aligner"], c["type"], c["score"]) for c in cases])
+    banded = [dict(aligner="gotoh", type="SEMI_GLOBAL", band=7, scheme=SCHEMES["gotoh"], pattern=PATTERN, text=TEXT,
+                   cigar="4M1D3M", score=implied_banded("4M1D3M", "gotoh", 7),
+                   source="NvB/nvbio-test/alignment_test.cu:790 (SingleTest::banded, :296-356)")]
+    json.dump({"alignment": cases, "edit_distance": ed, "banded": banded}, open(OUT, "w"), indent=1)
+    print(OUT, [(c["aligner"], c["type"], c["score"]) for c in cases + banded])
 
 
 if __name__ == "__main__":

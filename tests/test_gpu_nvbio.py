@@ -257,3 +257,66 @@ def test_reference_known_answers(engine):
     Tx = G.PackedSet.pack([G.ref2_codes(c["text"]) for c in ed], bits=2, big_endian=False)
     got = engine.nv_score_host(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), P, Tx)
     assert list(got) == [c["score"] for c in ed]
+
+
+# ---- BatchedBandedAlignmentScore<band> (gasalx_nv_banded_score_*, nvbanded.hpp) ----
+def _check_banded(engine, al, band, P, T):
+    g = engine.nv_banded_score_host(al, band, P, T)
+    o = O.nv_banded_score(al, band, P, T)
+    bad = np.nonzero(g != o)[0]
+    assert bad.size == 0, f"band {band}: {bad.size}/{len(g)} differ, first #{bad[0]}: gpu={g[bad[0]]} oracle={o[bad[0]]} {al}"
+    return g
+
+
+@pytest.mark.parametrize("base", ALIGNERS, ids=["gotoh", "sw", "ed", "gotoh_b"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_banded_per_pair_texts(engine, base, type_):
+    # reads against windows a few symbols longer (the banded use: a candidate location),
+    # every band-length instance (<= 8, <= 16, <= 32) at and inside its edges
+    rng = np.random.default_rng(300 + 7 * base.aligner + type_)
+    pats, texts = [], []
+    for _ in range(1500):
+        m = int(rng.integers(0, 200))
+        t = list(rng.integers(0, 4, max(0, m + int(rng.integers(-3, 40)))))
+        texts.append(np.array(t, np.uint32))
+        pats.append(np.array(_related(rng, t, m), np.uint32))
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+    for band in (2, 5, 7, 8, 9, 16, 17, 31, 32):
+        _check_banded(engine, _al(base, type_), band, P, T)
+
+
+@pytest.mark.parametrize("bits,big", [(2, True), (4, False), (8, True), (8, False)])
+def test_banded_packings_and_shared_text(engine, bits, big):
+    rng = np.random.default_rng(40 + bits + big)
+    hi = 4 if bits == 2 else (16 if bits == 4 else 256)
+    pats = [rng.integers(0, hi, int(rng.integers(0, 120))).astype(np.uint32) for _ in range(600)]
+    texts = [rng.integers(0, hi, int(rng.integers(0, 160))).astype(np.uint32) for _ in range(600)]
+    P, T = G.PackedSet.pack(pats, bits, big), G.PackedSet.pack(texts, bits, big)
+    shared = G.PackedSet.pack([rng.integers(0, hi, 300).astype(np.uint32)], bits, big, shared=True)
+    for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+        for band in (4, 12, 32):
+            _check_banded(engine, _al(ALIGNERS[0], type_), band, P, T)
+            _check_banded(engine, _al(ALIGNERS[1], type_), band, P, shared)
+
+
+def test_banded_reference_known_answers(engine):
+    # alignment_test.cu:680-745 (band 5 edit distance) and :790 (band 7 Gotoh semi-global)
+    import test_nvbio_oracle as TN
+    kats = TN._ref_kats()
+    for c in kats["edit_distance"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        assert int(engine.nv_banded_score_host(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), 5, P, T)[0]) == c["score"], c
+    (c,) = kats["banded"]
+    P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+    T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+    assert int(engine.nv_banded_score_host(TN.ref_aligner(c), 7, P, T)[0]) == c["score"]
+
+
+def test_banded_rejects_bad_band(engine):
+    P = G.PackedSet.pack([np.zeros(4, np.uint32)])
+    with pytest.raises(RuntimeError, match="band length"):
+        engine.nv_banded_score_host(ALIGNERS[0], 33, P, P)
+    with pytest.raises(RuntimeError, match="band length"):
+        engine.nv_banded_score_host(ALIGNERS[0], 1, P, P)

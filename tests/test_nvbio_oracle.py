@@ -150,3 +150,109 @@ def test_reference_edit_distance_cases():
     # full DP: every stated optimum lies inside the band, so the full DP agrees
     for c in _ref_kats()["edit_distance"]:
         assert score(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), c["pattern"], c["text"]) == c["score"], c
+
+
+# ---- banded front-end (BatchedBandedAlignmentScore<band>, orc_nv_banded_*) ----
+INT32_MIN = -(1 << 31)
+
+
+def banded_textbook(aligner, type_, p, t, band, s):
+    """Independent restatement of nvbio's banded DP over full-matrix cells (i, c) with
+    0 <= c - i < band (sw_banded_inl.h / gotoh_banded_inl.h, written here as a 2-D
+    recurrence): row -1 holds cells c = -1 .. band - 2; a cell's "top" is (i - 1, c)
+    (deletion, Gotoh F) when that cell is in the band, its "left" (i, c - 1)
+    (insertion, Gotoh E) when c - 1 >= i; text symbols past the end compare as 255."""
+    match, mismatch, go, ge, dl, ins = s
+    if aligner == G.NV_ED:
+        match, mismatch, dl, ins = 0, -1, -1, -1
+    M, N, B = len(p), len(t), band
+    if N < M:
+        return INT32_MIN
+    inf = -32768 - max(go, ge)
+    H, F = {}, {}
+    for c in range(-1, B - 1):
+        j = c + 1
+        if aligner == G.NV_GOTOH:
+            H[(-1, c)] = 0 if j == 0 else (go + (j - 1) * ge if type_ == G.NV_GLOBAL else 0)
+        else:
+            H[(-1, c)] = j * dl if type_ == G.NV_GLOBAL else 0
+        F[(-1, c)] = inf
+    best = INT32_MIN
+    for i in range(M):
+        E = None
+        for c in range(i, i + B):
+            sym = t[c] if c < N else 255
+            diag = H[(i - 1, c - 1)] + (match if sym == p[i] else mismatch)
+            has_top, has_left = c - (i - 1) < B, c - 1 >= i
+            if aligner == G.NV_GOTOH:
+                F[(i, c)] = max(F[(i - 1, c)] + ge, H[(i - 1, c)] + go) if has_top else inf
+                cand = [diag, F[(i, c)]] + ([E] if has_left else [])
+            else:
+                cand = [diag] + ([H[(i - 1, c)] + dl] if has_top else []) + ([H[(i, c - 1)] + ins] if has_left else [])
+            h = max(cand)
+            if type_ == G.NV_LOCAL:
+                h = max(h, 0)
+                best = max(best, h)
+            H[(i, c)] = h
+            if aligner == G.NV_GOTOH:
+                E = h + go if E is None else max(h + go, E + ge)
+    last = M - 1
+    if type_ == G.NV_GLOBAL:
+        best = max(best, H[(last, last + B - 1)])
+    elif type_ == G.NV_SEMI_GLOBAL:
+        m = (min(M + B - 1, N) - (M - 1)) % (1 << 32)
+        for j in range(B):
+            if j == 0 or j < m:
+                best = max(best, H[(last, last + j)])
+    return best
+
+
+def banded_score(al, band, p, t):
+    P = G.PackedSet.pack([np.array(p, np.uint32)], bits=4)
+    T = G.PackedSet.pack([np.array(t, np.uint32)], bits=2, big_endian=False)
+    return int(O.nv_banded_score(al, band, P, T)[0])
+
+
+def test_reference_banded_edit_distance_cases():
+    # alignment_test.cu:680-745: banded_alignment_score<5>(edit distance, SEMI_GLOBAL) against
+    # the stated scores, on the banded restatement itself
+    for c in _ref_kats()["edit_distance"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        got = int(O.nv_banded_score(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), c["band"], P, T)[0])
+        assert got == c["score"], c
+
+
+def test_reference_banded_gotoh_case():
+    # alignment_test.cu:790: the band-7 Gotoh SEMI_GLOBAL run whose traceback is 4M1D3M; its
+    # score is that CIGAR's best in-band placement (make_nvbio_reference_kats.py)
+    (c,) = _ref_kats()["banded"]
+    P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+    T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+    assert int(O.nv_banded_score(ref_aligner(c), c["band"], P, T)[0]) == c["score"] == 10
+
+
+@pytest.mark.parametrize("aligner,s", [(G.NV_GOTOH, (2, -1, -2, -1, 0, 0)), (G.NV_SW, (2, -3, 0, 0, -2, -3)),
+                                       (G.NV_ED, (0, 0, 0, 0, 0, 0)), (G.NV_GOTOH, (1, -4, -6, -1, 0, 0)),
+                                       (G.NV_SW, (1, 2, 0, 0, 1, -1))])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL])
+def test_banded_matches_textbook(aligner, s, type_):
+    rng = np.random.default_rng(1000 + 10 * aligner + type_)
+    al = G.NvAligner(aligner, type_, *s)
+    for band in (2, 3, 5, 7, 8, 13, 32):
+        for _ in range(12):
+            M = int(rng.integers(0, 24))
+            N = max(0, M + int(rng.integers(-2, 3 * band)))
+            p = [int(x) for x in rng.integers(0, 4, M)]
+            t = [int(x) for x in rng.integers(0, 4, N)]
+            for k in range(min(M, N)):
+                if rng.random() < 0.7:
+                    t[min(N - 1, k + band // 3)] = p[k]
+            if N < band - 1:
+                continue   # the reference's first-band load reads past such a text (nvbio_oracle.c)
+            assert banded_score(al, band, p, t) == banded_textbook(aligner, type_, p, t, band, s), (band, p, t)
+
+
+def test_banded_short_text_is_skipped():
+    al = G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2, -1, -2, -1)
+    assert banded_score(al, 5, [0, 1, 2, 3], [0, 1, 2]) == INT32_MIN
