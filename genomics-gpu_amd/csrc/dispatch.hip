@@ -959,6 +959,33 @@ static HmmFn hmm_lookup(int G) {
     }
 }
 
+// Two problems per lane group (pairhmm2_kernel): an A/B build only (-DGX_HMM2_BUILD=1,
+// then GASALX_HMM2=1 selects it).  Measured slower than one problem per group: 254
+// VGPRs hold it to 2 waves per SIMD (profiles/r03_pairhmm_ab.md).
+#ifndef GX_HMM2_BUILD
+#define GX_HMM2_BUILD 0
+#endif
+template <bool QUALS, bool ABS>
+static HmmFn hmm2_lookup(int G) {
+#if !GX_HMM2_BUILD
+    (void)G;
+    return nullptr;
+#else
+    switch (G) {
+        case 4: return &pairhmm2_kernel<4, kHmmRows, QUALS, ABS>;
+        case 8: return &pairhmm2_kernel<8, kHmmRows, QUALS, ABS>;
+        case 16: return &pairhmm2_kernel<16, kHmmRows, QUALS, ABS>;
+        case 32: return &pairhmm2_kernel<32, kHmmRows, QUALS, ABS>;
+        case 64: return &pairhmm2_kernel<64, kHmmRows, QUALS, ABS>;
+        default: return nullptr;
+    }
+#endif
+}
+static bool hmm2_wanted() {
+    static const bool on = GX_HMM2_BUILD && env_flag("GASALX_HMM2", false);
+    return on;
+}
+
 // lanes per pair for a read of max_r rows: kHmmRows (8) rows per lane, G in {4, ..., 64}
 int pairhmm_group(uint32_t max_r) {
     for (int g : {4, 8, 16, 32, 64})
@@ -978,14 +1005,18 @@ static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0,
     // reads shorter than the group's rows: the top lane's first row is virtual and
     // absorbs the boundary (pairhmm.hpp ABS)
     const bool absorb = (uint32_t)G * kHmmRows > max_r;
-    HmmFn fn = quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
-                     : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G));
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
-    // kHmmRows rows x 64 lanes x 4 bytes
-    const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * kHmmRows * 64 * 4;
+    // kHmmRows rows x 64 lanes x 4 bytes, per problem of a lane group
+    const int per_group = hmm2_wanted() ? 2 : 1;
+    const size_t lds = (((size_t)4 * per_group * (64 / G) * A.lds_stride + 15) & ~(size_t)15) +
+                       (size_t)per_group * 4 * 4 * kHmmRows * 64 * 4;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
+    HmmFn fn = per_group == 2 ? (quals ? (absorb ? hmm2_lookup<true, true>(G) : hmm2_lookup<true, false>(G))
+                                       : (absorb ? hmm2_lookup<false, true>(G) : hmm2_lookup<false, false>(G)))
+                              : (quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
+                                       : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G)));
     if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);
+    hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * per_group * (64 / G))), dim3(256), lds, st, A);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }
