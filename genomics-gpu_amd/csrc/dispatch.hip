@@ -623,8 +623,60 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     // walk (tb_kernel) bound by the latency of its dependent loads.  Chunk k's DP runs
     // on the caller's stream, its walk on a second stream after an event, beside the
     // following DPs.  Every chunk has its own workspace (direction data, flags, ends).
-    const uint32_t chunks = runs_tb && out.cigar && out.n_cigar_ops && shape.tb_split && pl.kind == PLAN_WAVEFRONT &&
-                                    !pl.need_pack ? tb_chunks(n) : 1;
+    const bool can_split = runs_tb && out.cigar && out.n_cigar_ops && shape.tb_split && pl.kind == PLAN_WAVEFRONT &&
+                           !pl.need_pack;
+    // Tail split (GASALX_TB_TAIL=1, A/B): the pairs that fill whole rounds of the packed
+    // DP kernel's wave slots, then the rest.  Chunk 0's walk runs on the second stream
+    // beside chunk 1's DP (the DP's last, partly filled round), chunk 1's walk follows
+    // its DP on the caller's stream.
+    if (can_split && pl.packed16 && env_flag("GASALX_TB_TAIL", false)) {
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ws.device));
+        const uint32_t per_wave = 2u * (64u / (uint32_t)pl.G16), waves_simd = 2;   // GX_WF16_TB_WAVES / _LTB_WAVES
+        const uint64_t round = (uint64_t)cus * 4 * waves_simd * per_wave;
+        const uint32_t n0 = round ? (uint32_t)((n / round) * round) : 0;
+        if (n0 > 0 && n0 < n) {
+            if (ws.sides.empty()) ws.sides.push_back(new Workspace());
+            ws.sides[0]->device = ws.device;
+            if (!ws.walk_stream) HIPCHK(hipStreamCreateWithFlags(&ws.walk_stream, hipStreamNonBlocking));
+            for (hipEvent_t *x : {&ws.fork, &ws.join, &ws.dp_done})
+                if (!*x) HIPCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ws.fork, st));
+            HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.fork, 0));
+            int rc = GASALX_OK;
+            for (uint32_t c = 0; c < 2 && rc == GASALX_OK; c++) {
+                const uint32_t i0 = c ? n0 : 0, m = c ? n - n0 : n0;
+                gasalx_batch cb = b;
+                cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
+                if (cb.q_ops) cb.q_ops += i0;
+                if (cb.t_ops) cb.t_ops += i0;
+                if (cb.seed_scores) cb.seed_scores += i0;
+                cb.n_alns = m;
+                gasalx_results co = out;
+                for (int32_t **f : {&co.aln_score, &co.q_end, &co.t_end, &co.q_start, &co.t_start, &co.aln_score2,
+                                    &co.q_end2, &co.t_end2})
+                    if (*f) *f += i0;
+                co.n_cigar_ops += i0;
+                BatchShape cs = sized;
+                cs.n = m;
+                const Plan cp = make_plan(p, cs, has_ops);
+                Workspace &w = c ? *ws.sides[0] : ws;
+                rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_DP);
+                if (rc) break;
+                if (c == 0) {
+                    HIPCHK(hipEventRecord(ws.dp_done, st));
+                    HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.dp_done, 0));
+                    rc = align_body(w, p, cp, cb, co, ws.walk_stream, cs, cigar_cap, walk_qseq, PHASE_WALK);
+                } else {
+                    rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_WALK);
+                }
+            }
+            HIPCHK(hipEventRecord(ws.join, ws.walk_stream));
+            HIPCHK(hipStreamWaitEvent(st, ws.join, 0));
+            return rc;
+        }
+    }
+    const uint32_t chunks = can_split ? tb_chunks(n) : 1;
     if (chunks > 1) {
         while (ws.sides.size() + 1 < chunks) ws.sides.push_back(new Workspace());
         for (Workspace *w : ws.sides) w->device = ws.device;
