@@ -13,6 +13,7 @@
 #include "engine.hpp"
 #include "generic.hpp"
 #include "pairhmm.hpp"
+#include "ksw16.hpp"
 #include "start.hpp"
 #include "wavefront.hpp"
 #include "wavefront16.hpp"
@@ -867,6 +868,32 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                 HIPCHK(ws.misc.reserve(n));
                 HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
                 todo = ws.misc.as<uint8_t>();
+                // two pairs per lane in 16-bit halves first (ksw16.hpp): the pairs it takes
+                // get todo = 0xFF, the rest run the levels below (GASALX_KSW16=0: levels only)
+                const int32_t nsc = p.has_n_penalty ? -p.n_penalty : 0;
+                const int32_t kofs = std::max({0, p.mismatch, -nsc, -p.match});
+                const bool k16 = env_flag("GASALX_KSW16", true) && p.gap_open >= 0 && p.gap_extend >= 0 &&
+                                 p.gap_open + p.gap_extend <= 0x300 && p.match + kofs <= 255 &&
+                                 -p.mismatch + kofs <= 255 && nsc + kofs <= 255 && shape.max_q <= 254;
+                if (k16) {
+                    Ksw16Args K;
+                    std::memset(&K, 0, sizeof(K));
+                    K.qw = A.qw; K.tw = A.tw;
+                    K.qoff = b.q_offsets; K.toff = b.t_offsets; K.qlen = b.q_lens; K.tlen = b.t_lens;
+                    K.seed = b.seed_scores;
+                    K.score = out.aln_score; K.qend = qend; K.tend = tend;
+                    K.todo = todo;
+                    K.n = n; K.n_lanes = (n + 1) / 2; K.cols = (shape.max_q + 3) & ~1u;
+                    K.stride = grid_for(K.n_lanes, 256) * 256;
+                    const size_t ent_words = (size_t)K.cols * K.stride, sel_words = (size_t)(K.cols / 2) * K.stride;
+                    HIPCHK(ws.rows_e.reserve((ent_words + sel_words) * 4 + 64));
+                    K.ent = ws.rows_e.as<uint32_t>(); K.sel = K.ent + ent_words;
+                    K.a = p.match; K.b = p.mismatch; K.o = p.gap_open; K.e = p.gap_extend;
+                    K.nval = p.n_code & 0xF; K.has_npen = p.has_n_penalty; K.npen = p.n_penalty;
+                    K.kofs = kofs;
+                    ksw16_kernel<<<grid_for(K.n_lanes, 256), 256, 0, st>>>(K);
+                    HIPCHK(hipGetLastError());
+                }
                 // level 0 with the entries in LDS when two blocks of >= 64 threads fit
                 // a CU, for batches of up to 4 waves per SIMD: LDS then holds 2 waves
                 // per SIMD, and larger batches run faster on the global array with its

@@ -1168,3 +1168,24 @@ def test_semiglobal_tail_query_equals_int32_kernel(engine, monkeypatch):
     r32 = engine.align_host(b, G.make_params(**kw))
     for f in ("score", "q_end", "t_end"):
         assert np.array_equal(r16[f], r32[f]), f
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(match=2, mismatch=3, gap_open=5, gap_extend=2), dict(n_penalty=2)])
+def test_ksw16_equals_levels(engine, monkeypatch, kw):
+    # two pairs per lane (ksw16.hpp) against the thread-per-pair levels on config-2 data with
+    # N in a tenth of the targets (queries with N stay on the levels), odd pair count
+    b = G.Batch.synth(2, 20001, 0x5EED0216)
+    rng = np.random.default_rng(216)
+    for k in rng.choice(b.n, b.n // 10, replace=False):
+        o = int(b.t_offsets[k]) + int(rng.integers(0, int(b.t_lens[k])))
+        b.t_data[o] = ord("N")
+    seed = rng.integers(0, 40, b.n).astype(np.uint32)
+    p = G.make_params(algo=G.KSW, **kw)
+    r16 = engine.align_host(b, p, seed_scores=seed)
+    monkeypatch.setenv("GASALX_KSW16", "0")
+    r32 = engine.align_host(b, p, seed_scores=seed)
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(r16[f], r32[f]), f
+    o = O.align(b, O.make_params(algo=G.KSW, **kw), seed_scores=seed)
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(r16[f], o[f]), f
