@@ -885,13 +885,28 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                     K.todo = todo;
                     K.n = n; K.n_lanes = (n + 1) / 2; K.cols = (shape.max_q + 3) & ~1u;
                     K.stride = grid_for(K.n_lanes, 256) * 256;
-                    const size_t ent_words = (size_t)K.cols * K.stride, sel_words = (size_t)(K.cols / 2) * K.stride;
-                    HIPCHK(ws.rows_e.reserve((ent_words + sel_words) * 4 + 64));
-                    K.ent = ws.rows_e.as<uint32_t>(); K.sel = K.ent + ent_words;
                     K.a = p.match; K.b = p.mismatch; K.o = p.gap_open; K.e = p.gap_extend;
                     K.nval = p.n_code & 0xF; K.has_npen = p.has_n_penalty; K.npen = p.n_penalty;
                     K.kofs = kofs;
-                    ksw16_kernel<<<grid_for(K.n_lanes, 256), 256, 0, st>>>(K);
+                    // the entry row in registers when the padded query fits an instance
+                    // (selector words in LDS: QC / 2 words per lane), else the global array
+                    // (GASALX_KSW16_REG=0: global, A/B)
+                    int qc = 0;
+                    if (env_flag("GASALX_KSW16_REG", true))
+                        for (int c : {64, 96, 160})
+                            if (K.cols <= (uint32_t)c) { qc = c; break; }
+                    if (qc) {
+                        void (*fn)(Ksw16Args) = qc == 64 ? &ksw16_kernel<64> : qc == 96 ? &ksw16_kernel<96> : &ksw16_kernel<160>;
+                        const size_t lds = (size_t)4 * (qc / 2) * 64 * 4;
+                        if (lds > 64 * 1024)
+                            HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                        hipLaunchKernelGGL(fn, dim3(grid_for(K.n_lanes, 256)), dim3(256), lds, st, K);
+                    } else {
+                        const size_t ent_words = (size_t)K.cols * K.stride, sel_words = (size_t)(K.cols / 2) * K.stride;
+                        HIPCHK(ws.rows_e.reserve((ent_words + sel_words) * 4 + 64));
+                        K.ent = ws.rows_e.as<uint32_t>(); K.sel = K.ent + ent_words;
+                        ksw16_kernel<0><<<grid_for(K.n_lanes, 256), 256, 0, st>>>(K);
+                    }
                     HIPCHK(hipGetLastError());
                 }
                 // level 0 with the entries in LDS when two blocks of >= 64 threads fit

@@ -73,7 +73,14 @@ __device__ __forceinline__ uint32_t ksw16_first_row(uint32_t j, uint32_t h0, int
 #ifndef GX_KSW16_WAVES
 #define GX_KSW16_WAVES 8   // waves per SIMD the register allocator must allow (A/B: 7)
 #endif
-__global__ __launch_bounds__(256, GX_KSW16_WAVES) void ksw16_kernel(Ksw16Args A) {
+// QC = 0: entries in the global [column][lane] array (any query up to 254).  QC > 0: the
+// row of entries in QC registers of the lane and the selector words in LDS
+// ([wave][column / 2][lane]), for queries up to QC - 2: no entry traffic at all (the
+// global form moves ~84 GB per 1 M config-2 pairs and is HBM-bound, profiles/r03_ksw16.md).
+template <int QC>
+__global__ __launch_bounds__(256, QC == 0 ? GX_KSW16_WAVES : QC <= 64 ? 4 : QC <= 128 ? 3 : 2) void ksw16_kernel(Ksw16Args A) {
+    extern __shared__ uint32_t ksw16_lds[];
+    constexpr bool REG = QC > 0;
     const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
     constexpr uint32_t BIAS = 0x0800u, BIAS2 = 0x08000800u;
     const int32_t oe = A.o + A.e;
@@ -106,7 +113,9 @@ __global__ __launch_bounds__(256, GX_KSW16_WAVES) void ksw16_kernel(Ksw16Args A)
     qmax = (uint32_t)ksw_wave_max((int)qmax);
     const uint32_t stride = A.stride;                    // >= every lane of the grid
     uint32_t *ent = A.ent + lane_id;
-    uint32_t *selp = A.sel + lane_id;
+    uint32_t *selp = REG ? ksw16_lds + (threadIdx.x >> 6) * (QC / 2) * 64 + (threadIdx.x & 63) : A.sel + lane_id;
+    const uint32_t sstride = REG ? 64u : stride;
+    uint32_t reg[REG ? QC : 1];
     // ---- selector words and the first row ----
     {
         for (uint32_t j = 0; j < qmax + 2; j += 2) {
@@ -119,14 +128,37 @@ __global__ __launch_bounds__(256, GX_KSW16_WAVES) void ksw16_kernel(Ksw16Args A)
                 if (act_pair[1] && jj < ql[1]) cB = ksw16_code((A.qw[qo[1] + (jj >> 3)] >> (28 - 4 * (jj & 7))) & 15u);
                 s |= (cA | ((4u + cB) << 8)) << (16 * u);
             }
-            if (j / 2 < (A.cols + 1) / 2) selp[(size_t)(j / 2) * stride] = s;
+            if (j / 2 < (A.cols + 1) / 2) selp[(size_t)(j / 2) * sstride] = s;
         }
-        for (uint32_t j = 0; j < qmax + 2 && j < A.cols; ++j) {
-            uint32_t w = 0;
+        if constexpr (REG) {
+            // eh[0] = h0, eh[1] = v1 = max(h0 - oe, 0), eh[j] = eh[j-1] - e while eh[j-1] > e and
+            // j <= qlen: eh[j] = v1 - (j-1)e where j <= qlen and v1 > (j-1)e, else 0 (closed form)
+            int32_t v1[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (act_pair[h]) w |= ksw16_first_row(j, h0[h], oe, A.e, ql[h]) << (16 * h);
-            ent[(size_t)j * stride] = w;
+            for (int h = 0; h < 2; ++h) v1[h] = act_pair[h] ? max((int32_t)h0[h] - oe, 0) : 0;
+#pragma unroll
+            for (int j = 0; j < QC; ++j) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    int32_t v;
+                    if (j == 0) v = act_pair[h] ? (int32_t)h0[h] : 0;
+                    else {
+                        const int32_t t = v1[h] - (j - 1) * A.e;
+                        v = ((uint32_t)j <= ql[h] && t > 0) ? t : 0;
+                    }
+                    w |= (uint32_t)v << (16 * h);
+                }
+                reg[j] = w;
+            }
+        } else {
+            for (uint32_t j = 0; j < qmax + 2 && j < A.cols; ++j) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (act_pair[h]) w |= ksw16_first_row(j, h0[h], oe, A.e, ql[h]) << (16 * h);
+                ent[(size_t)j * stride] = w;
+            }
         }
     }
     // ---- per-half row state (the reference's scalars) ----
@@ -192,8 +224,8 @@ __global__ __launch_bounds__(256, GX_KSW16_WAVES) void ksw16_kernel(Ksw16Args A)
         const int j0 = __builtin_amdgcn_readfirstlane(jlo) & ~1, j1 = __builtin_amdgcn_readfirstlane(jhi);
         uint32_t JP = (uint32_t)(j0 + 1) * 0x10001u;          // j + 1 per half
         uint32_t *pe = ent + (size_t)j0 * stride;
-        const uint32_t *ps = selp + (size_t)(j0 >> 1) * stride;
-        auto cell = [&](const uint32_t w, const uint32_t selw, uint32_t *dst) {
+        const uint32_t *ps = selp + (size_t)(j0 >> 1) * sstride;
+        auto cell = [&](const uint32_t w, const uint32_t selw, uint32_t &dst) {
             const uint32_t H2 = __builtin_amdgcn_perm(0x08080808u, w, 0x04020400u);   // {hA, 8, hB, 8}: h + 0x800
             const uint32_t E2 = __builtin_amdgcn_perm(0x08080808u, w, 0x04030401u);
             const uint32_t nzM = l16_nz_mask(w & 0x00FF00FFu);                       // [H(i-1, j-1) != 0]
@@ -214,29 +246,47 @@ __global__ __launch_bounds__(256, GX_KSW16_WAVES) void ksw16_kernel(Ksw16Args A)
             const uint32_t wn = __builtin_amdgcn_perm(En & lt16, H1, 0x06020400u);
             const uint32_t mle = __builtin_amdgcn_perm(d2, d2, 0x09090808u);
             const uint32_t ws = __builtin_amdgcn_bitop3_b32(wn, w, mle, 0xE4);        // le ? wn : w
-            *dst = ws;
+            dst = ws;
             const uint32_t nz = l16_nz_mask(ws);
             first2 = pk_min_u16(first2, JP | ~nz);
             last2 = pk_max_u16(last2, JP & nz);
-            H1 = Hn;
+            // H1 stops at the half's last cell: the stored h at j == end is H(i, end-1), and
+            // after the row H1 holds it for the Q16 rule
+            H1 = __builtin_amdgcn_bitop3_b32(Hn, H1, lt16, 0xE4);                   // lt ? Hn : H1
             JP += 0x10001u;
         };
-        for (int j = j0; j <= j1; j += 2) {
-            const uint32_t sw = *ps;
-            const uint32_t w0 = pe[0], w1 = pe[stride];
-            cell(w0, __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04010400u), pe);
-            cell(w1, __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04030402u), pe + stride);
-            pe += 2 * stride;
-            ps += stride;
+        if constexpr (REG) {
+            // blocks of 8 columns, unrolled over the register row; blocks wholly outside
+            // [j0, j1] are skipped (wave-uniform branch)
+#pragma unroll
+            for (int blk = 0; blk < QC / 8; ++blk) {
+                if (blk * 8 + 7 < j0 || blk * 8 > j1) continue;
+                JP = (uint32_t)(blk * 8 + 1) * 0x10001u;
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    const int j = blk * 8 + k;
+                    const uint32_t sw = selp[(j >> 1) * 64];
+                    cell(reg[j], __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04010400u), reg[j]);
+                    cell(reg[j + 1], __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04030402u), reg[j + 1]);
+                }
+            }
+        } else {
+            for (int j = j0; j <= j1; j += 2) {
+                const uint32_t sw = *ps;
+                const uint32_t w0 = pe[0], w1 = pe[stride];
+                cell(w0, __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04010400u), pe[0]);
+                cell(w1, __builtin_amdgcn_perm(0x0C0C0C0Cu, sw, 0x04030402u), pe[stride]);
+                pe += 2 * stride;
+                ps += sstride;
+            }
         }
         // ---- row end per half (ksw_kernel_template.h:160-186) ----
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (!act[h]) continue;
             const int32_t e_ = end[h];
-            // H(i, end-1) is the h byte stored at eh[end]
-            const uint32_t wend = ent[(size_t)e_ * stride];
-            const int32_t h1 = (int32_t)((wend >> (16 * h)) & 0xFFu);
+            // H(i, end-1): H1 stopped at the half's last cell (biased)
+            const int32_t h1 = (int32_t)((H1 >> (16 * h)) & 0xFFFFu) - (int32_t)BIAS;
             if (e_ == (int32_t)ql[h] || (ql[h] & 7u) == 0) {                   // Q16
                 mx_ie[h] = gsc[h] > h1 ? mx_ie[h] : i;
                 gsc[h] = gsc[h] > h1 ? gsc[h] : h1;
