@@ -86,6 +86,11 @@ WORKLOADS = {
                                "Gotoh (2,-1,-2,-1) semi-global, 1M 150bp reads (4-bit DNA_N) per GPU, each against "
                                "its 165bp reference window (2-bit) starting 7bp before the read's origin; cells = "
                                "the band's (150 x 16 per pair), seed 0x5EED0006"),
+    "ksw": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.KSW), bytes=340, ops=14, packed=True,
+                seed_score=10,
+                label="GASAL2 KSW (ksw_kernel_template.h:47-199, BWA ksw_extend semantics) on config-2 data, 1M "
+                      "pairs x 150bp per GPU, seed score 10 per pair; cells = the full rectangle (the kernel "
+                      "trims, as the reference does)"),
     "cpu_plumbing": dict(kind=1, pairs=1024, scaling="weak", params=dict(algo=G.LOCAL), bytes=152, ops=12,
                          label="config1: 1024 pairs 64x64 SW local through the host-side CPU verify scorer "
                                "(oracle/), same batch through the GPU, seed 0x5EED0001"),
@@ -95,6 +100,7 @@ METRICS = {
     "nvbio_gotoh": "GCUPS of nvbio-style batched Gotoh semi-global scoring (sw-benchmark idiom) on MI355X",
     "nvbio_banded": "GCUPS (band cells) of nvbio-style banded (16) Gotoh semi-global scoring on MI355X",
     "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
+    "ksw": "GCUPS of GASAL2 KSW extension (config-2 data, 1M x 150bp) on MI355X",
 }
 SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006}
 
@@ -298,8 +304,9 @@ def host_info():
     return info
 
 
-def oracle_align(O, batch, pkw, threads):
-    return O.align(batch, O.make_params(**pkw), n_threads=threads)
+def oracle_align(O, batch, pkw, threads, seed_score=None):
+    seeds = None if seed_score is None else np.full(batch.n, seed_score, np.uint32)
+    return O.align(batch, O.make_params(**pkw), seed_scores=seeds, n_threads=threads)
 
 
 def oracle_pairhmm(O, h, threads):
@@ -327,7 +334,7 @@ def band_cells_of(batch, k_band):
     return total
 
 
-def single_core_rate(O, kind, data, pkw, budget_s):
+def single_core_rate(O, kind, data, pkw, budget_s, seed_score=None):
     """The oracle on 1 thread over a prefix of the rank-0 shard, bounded by budget_s."""
     chunk = 256 if kind in (5, 6) else 4096
     done, cells, used = 0, 0, 0.0
@@ -354,7 +361,7 @@ def single_core_rate(O, kind, data, pkw, budget_s):
         else:
             sub = data.slice(done, e)
             t0 = time.perf_counter()
-            oracle_align(O, sub, pkw, 1)
+            oracle_align(O, sub, pkw, 1, seed_score)
             used += time.perf_counter() - t0
             cells += cells_of(sub)
         done = e
@@ -392,7 +399,7 @@ def compare_align(g, o, fields, batch=None, cigar=False):
 
 
 # ------------------------------------------------------------------ e2e -----
-def end_to_end(eng, kind, data, params, cells, reps=5):
+def end_to_end(eng, kind, data, params, cells, reps=5, seed_score=None):
     """PCIe-inclusive rate through the host-buffer entry point (gasalx_align_host /
     gasalx_pairhmm_host): host arrays in, H2D + kernels + D2H, results back in host
     arrays.  Reported beside `value`, never as it."""
@@ -412,7 +419,8 @@ def end_to_end(eng, kind, data, params, cells, reps=5):
         fields = ["score"] if params.algo == G.GLOBAL else ["score", "q_end", "t_end"]
         if params.start_pos == G.WITH_START:
             fields += ["q_start", "t_start"]
-        call = lambda: eng.align_host(data, params, fields=fields)
+        seeds = None if seed_score is None else np.full(data.n, seed_score, np.uint32)
+        call = lambda: eng.align_host(data, params, fields=fields, seed_scores=seeds)
         path = ("gasalx_align_host (pageable host arrays; chunks of pairs on two streams, "
                 "H2D of chunk k+1 overlapping the kernels of chunk k)")
 
@@ -474,6 +482,9 @@ def dtype_label(plan, kind):
         return "int16x2 packed (two pairs per lane, exact value window), int32 fallback per declined pair"
     if plan.startswith("wavefront_"):
         return "int32"
+    if plan == "generic_ksw":
+        return ("int8 (h, e) entries, int16x2 packed arithmetic (ksw16: two pairs per lane, exact 8-bit bound), "
+                "thread-per-pair 8/16/32-bit levels per declined pair")
     return "int32 (int16 row buffer, as the reference)"
 
 
@@ -647,6 +658,8 @@ def main():
             d["q_start"] = torch.empty(n, dtype=torch.int32, device=dev)
             d["t_start"] = torch.empty(n, dtype=torch.int32, device=dev)
             fields += ["q_start", "t_start"]
+        if wl.get("seed_score") is not None:     # KSW: the seed score of every pair
+            d["seed_scores"] = torch.full((n,), wl["seed_score"], dtype=torch.int32, device=dev)
         tb = pkw.get("start_pos") == G.WITH_TB
         if tb:
             d["cigar"] = torch.empty(batch.q_bytes, dtype=torch.uint8, device=dev)
@@ -709,10 +722,10 @@ def main():
     if world == 1 and not args.no_cpu and O is not None:
         # the CPU baseline: both builds of the oracle on a 1-core sample (half the budget
         # each), the faster one then times the 16-thread parity run
-        builds = {"portable": single_core_rate(O, kind, data, pkw, args.cpu_seconds / 2)}
+        builds = {"portable": single_core_rate(O, kind, data, pkw, args.cpu_seconds / 2, wl.get("seed_score"))}
         if O.NATIVE_OK:
             O.use_native(True)
-            builds["native"] = single_core_rate(O, kind, data, pkw, args.cpu_seconds / 2)
+            builds["native"] = single_core_rate(O, kind, data, pkw, args.cpu_seconds / 2, wl.get("seed_score"))
             O.use_native(builds["native"]["value"] >= builds["portable"]["value"])
     if args.parity_pairs > 0:
         m = min(n, args.parity_pairs)
@@ -732,7 +745,7 @@ def main():
             ref_scores = ref
         else:
             sub = data.slice(0, m)
-            ref = oracle_align(O, sub, pkw, threads)
+            ref = oracle_align(O, sub, pkw, threads, wl.get("seed_score"))
             gsub = {f: got[f][:m] for f in fields}
             if tb:
                 gsub["cigar"] = got["cigar"][:sub.q_bytes]
@@ -804,7 +817,7 @@ def main():
         same = (pmc is not None and pmc.get("pairs_per_launch") == n and pmc.get("plan") == plan and
                 pmc.get("lib_sha256") == sha and not probe)
         traffic = pmc.get("hbm_bytes_per_launch") if same else None
-        packed = plan.startswith(("wavefront16", "nvbio16"))
+        packed = plan.startswith(("wavefront16", "nvbio16")) or wl.get("packed", False)
         lane_rate = VALU_LANE_OPS * (2 if packed else 1)
         kcells = cells_per_step / kern_s
         if kind == 5:
@@ -881,7 +894,8 @@ def main():
             "vs_reference_a100_derived": round(gcups / world / 80.0, 2),
         }
         if world == 1 and not args.no_e2e:
-            out["end_to_end"] = end_to_end(eng, kind, data, None if kind in (5, 6) else params, cells_per_step)
+            out["end_to_end"] = end_to_end(eng, kind, data, None if kind in (5, 6) else params, cells_per_step,
+                                           seed_score=wl.get("seed_score"))
         if cpu is not None:
             out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
