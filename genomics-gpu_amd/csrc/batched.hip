@@ -216,10 +216,43 @@ NvBandFn nv_band_lookup_t(int type, uint32_t band) {
     return type == NV_GLOBAL ? nv_band_pick<ALN, NV_GLOBAL>(band)
          : type == NV_SEMI ? nv_band_pick<ALN, NV_SEMI>(band) : nv_band_pick<ALN, NV_LOCAL>(band);
 }
+using NvBand16Fn = void (*)(NvBand16Args);
+template <int ALN, int TYPE>
+NvBand16Fn nv_band16_pick(uint32_t band) {
+    if (band <= 8) return &nv_banded16_kernel<ALN, TYPE, 8>;
+    if (band <= 16) return &nv_banded16_kernel<ALN, TYPE, 16>;
+    if (band <= 32) return &nv_banded16_kernel<ALN, TYPE, 32>;
+    return nullptr;
+}
+template <int ALN>
+NvBand16Fn nv_band16_lookup_t(int type, uint32_t band) {
+    return type == NV_GLOBAL ? nv_band16_pick<ALN, NV_GLOBAL>(band)
+         : type == NV_SEMI ? nv_band16_pick<ALN, NV_SEMI>(band) : nv_band16_pick<ALN, NV_LOCAL>(band);
+}
+// the packed banded kernel: 2-bit texts, gaps <= 0, match - mismatch in a byte, every
+// value (bounded by (M + band + 2) * the largest score magnitude) inside the 16-bit f16
+// window (as nv16_ok); GASALX_NVB16=0: int32 only
+bool nvb16_ok(int32_t match, int32_t mismatch, int32_t go, int32_t ge, int32_t del, int32_t ins, uint32_t text_bits,
+              uint32_t max_p, uint32_t band, uint32_t *base) {
+    const char *env = std::getenv("GASALX_NVB16");
+    if (env && std::atoi(env) == 0) return false;
+    if (text_bits != 2) return false;
+    if (match < mismatch || match - mismatch > 255) return false;
+    if (go > 0 || ge > 0 || del > 0 || ins > 0) return false;
+    const int64_t mag = std::max<int64_t>({std::abs((int64_t)match), std::abs((int64_t)mismatch), std::abs((int64_t)go),
+                                           std::abs((int64_t)ge), std::abs((int64_t)del), std::abs((int64_t)ins), 1});
+    if (mag > 0x200) return false;
+    const int64_t vabs = ((int64_t)max_p + band + 2) * mag * 2;
+    const int64_t b = 0x400 + 2 * (std::abs((int64_t)go) + std::abs((int64_t)ge) + std::abs((int64_t)del) +
+                                   std::abs((int64_t)ins)) + vabs + 64;
+    if (b + vabs + 512 > 0x7BFF) return false;
+    *base = (uint32_t)b;
+    return true;
+}
 }  // namespace
 
 int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
-                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st) {
+                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st, uint32_t max_p) {
     if (al.aligner < 0 || al.aligner > 2 || al.type < 0 || al.type > 2) { set_error("bad aligner"); return GASALX_EINVAL; }
     if (band < 2 || band > 32) { set_error("band length must be 2..32"); return GASALX_EINVAL; }
     for (uint32_t b : {pat.bits, txt.bits})
@@ -234,6 +267,21 @@ int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t 
     if (al.aligner == NV_ED) { A.match = 0; A.mismatch = -1; A.del = -1; A.ins = -1; }   // ed_banded_inl.h:63-78
     else { A.match = al.match; A.mismatch = al.mismatch; A.del = al.deletion; A.ins = al.insertion; }
     A.go = al.gap_open; A.ge = al.gap_ext;
+    uint32_t base = 0;
+    if (max_p && nvb16_ok(A.match, A.mismatch, A.go, A.ge, A.del, A.ins, txt.bits, max_p, band, &base)) {
+        NvBand16Args D;
+        D.pw = A.pw; D.poff = A.poff; D.pbits = A.pbits; D.pbig = A.pbig;
+        D.tw = A.tw; D.toff = A.toff; D.tbig = A.tbig; D.tlen0 = A.tlen0;
+        D.score = scores; D.n = n; D.n_lanes = (n + 1) / 2; D.band = band;
+        D.match = A.match; D.mismatch = A.mismatch; D.go = A.go; D.ge = A.ge; D.del = A.del; D.ins = A.ins;
+        D.base = base;
+        NvBand16Fn f16 = al.aligner == NV_GOTOH ? nv_band16_lookup_t<NV_GOTOH>(al.type, band)
+                                                : nv_band16_lookup_t<NV_SW>(al.type, band);
+        hipLaunchKernelGGL(f16, dim3((D.n_lanes + 255) / 256), dim3(256), 0, st, D);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+        return GASALX_OK;
+    }
     NvBandFn fn = al.aligner == NV_GOTOH ? nv_band_lookup_t<NV_GOTOH>(al.type, band) : nv_band_lookup_t<NV_SW>(al.type, band);
     hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();

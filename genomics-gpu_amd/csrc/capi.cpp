@@ -595,10 +595,17 @@ int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32
 
 int gasalx_nv_banded_score_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
                                   const gasalx_nv_strings *pat, const gasalx_nv_strings *txt, int32_t *scores,
-                                  void *stream) {
+                                  uint32_t max_p, void *stream) {
     if (!eng || !al || !pat || !txt) { gx::set_error("null argument"); return GASALX_EINVAL; }
     CK(hipSetDevice(eng->device));
-    return gx::nv_banded_score_device(*al, band, n, *pat, *txt, scores, stream ? (hipStream_t)stream : eng->stream);
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    if (n && !max_p && pat->offsets) {   // read the offsets back (synchronises the stream)
+        std::vector<uint32_t> po(n + 1);
+        CK(hipMemcpyAsync(po.data(), pat->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        max_p = max_span(po.data(), n);
+    }
+    return gx::nv_banded_score_device(*al, band, n, *pat, *txt, scores, st, max_p);
 }
 
 int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
@@ -621,7 +628,7 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al,
     if ((rc = stage_in(eng->nv_to, txt->offsets, txt->offsets ? (size_t)n + 1 : 0, st, &p32))) return rc;
     dt.offsets = txt->offsets ? p32 : nullptr;
     CK(eng->nv_s.reserve((size_t)n * 4));
-    rc = gx::nv_banded_score_device(*al, band, n, dp, dt, eng->nv_s.as<int32_t>(), st);
+    rc = gx::nv_banded_score_device(*al, band, n, dp, dt, eng->nv_s.as<int32_t>(), st, max_span(pat->offsets, n));
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));

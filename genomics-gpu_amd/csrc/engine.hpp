@@ -114,8 +114,9 @@ int nv_score_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_str
                     const gasalx_nv_strings &txt, int32_t *scores, int16_t *scores16, uint32_t max_p, uint32_t max_t,
                     hipStream_t stream);
 // nvbio BatchedBandedAlignmentScore<band> (batched.hip / nvbanded.hpp): BestSink score per pair
+// max_p: the longest pattern (0: unknown; the packed kernel needs it for its value window)
 int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
-                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st);
+                           const gasalx_nv_strings &txt, int32_t *scores, hipStream_t st, uint32_t max_p);
 std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text,
                          uint32_t text_bits);
 

@@ -137,4 +137,160 @@ __global__ __launch_bounds__(256) void nv_banded_kernel(NvBandArgs A) {
     A.score[tid] = best;
 }
 
+
+// ---------------------------------------------------------------------------
+// Two pairs per lane in 16-bit halves (nv_banded16_kernel): slots 2t and 2t + 1 of the
+// batch share a lane, the band registers hold both pairs' cells (low / high half), the
+// arithmetic is nvbio16.hpp's: stored value = value + base inside the positive normal
+// f16 range, so v_pk_maximum3_f16 is an exact 3-way max of both pairs and 32-bit adds
+// never carry across halves; -inf is NEG = 0x0400, LOCAL floors E and F at 0 (exact
+// for H: gaps never score > 0).  Substitution: per row a 4-byte table per half,
+// byte t = [t == pattern symbol]·(match − mismatch) (symbols >= 4 select none), and a
+// per-band-slot selector {tA, 0x0C, 4 + tB, 0x0C} of the two texts' 2-bit symbols (past
+// a text's end: 0x0C, the constant 0, a mismatch as nvbio's 255); tmp = H + byte +
+// mismatch is one v_add3.  The halves may differ in length: the row loop runs to the
+// longer pattern and each half's sinks are taken at its own last row.
+// 2-bit texts, gap scores <= 0, match - mismatch <= 255 and the value window are the
+// host's conditions (batched.hip nvb16_ok); otherwise nv_banded_kernel runs.
+// ---------------------------------------------------------------------------
+struct NvBand16Args {
+    const uint32_t *pw, *poff;      // pattern words, n + 1 symbol offsets
+    uint32_t pbits, pbig;
+    const uint32_t *tw, *toff;      // 2-bit text words, n + 1 offsets (NULL: one shared text of tlen0)
+    uint32_t tbig, tlen0;
+    int32_t *score;
+    uint32_t n, n_lanes, band;
+    int32_t match, mismatch, go, ge, del, ins;
+    uint32_t base;                  // stored value of 0
+};
+
+template <int ALN, int TYPE, int BMAX>
+__global__ __launch_bounds__(256) void nv_banded16_kernel(NvBand16Args A) {
+    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= A.n_lanes) return;
+    constexpr bool GOTOH = ALN == NV_GOTOH;
+    const bool shared = A.toff == nullptr;
+    uint32_t M[2], N[2], po[2], to[2];
+    bool valid[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t pr = 2 * lane + h;
+        valid[h] = pr < A.n;
+        const uint32_t pp = valid[h] ? pr : 2 * lane;
+        po[h] = A.poff[pp]; M[h] = A.poff[pp + 1] - po[h];
+        to[h] = shared ? 0u : A.toff[pp];
+        N[h] = shared ? A.tlen0 : A.toff[pp + 1] - to[h];
+    }
+    const uint32_t Bn = A.band;
+    const int32_t Bs = (int32_t)A.base;
+    const uint32_t BB = A.base * 0x10001u, NEG = 0x04000400u;
+    const uint32_t FLOOR = TYPE == NV_LOCAL ? BB : NEG;
+    const uint32_t MIS = (uint32_t)A.mismatch * 0x10001u;
+    const uint32_t GO = (uint32_t)(-A.go) * 0x10001u, GE = (uint32_t)(-A.ge) * 0x10001u;   // gaps <= 0
+    const uint32_t DEL = (uint32_t)(-A.del) * 0x10001u, INS = (uint32_t)(-A.ins) * 0x10001u;
+    const uint32_t dm = (uint32_t)(A.match - A.mismatch);
+    uint32_t H[BMAX], F[BMAX], sel[BMAX];
+    NvSymReader tr[2], prd[2];
+    uint32_t tnext[2] = {0u, 0u};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        prd[h].init(A.pw, A.pbits, A.pbig, po[h], M[h]);
+        tr[h].init(A.tw, 2u, A.tbig, to[h], N[h]);
+    }
+    // text selector of the next symbol of each half: 2-bit code (high half + 4), or 0x0C past the end
+    auto next_sel = [&]() {
+        uint32_t sa = 0x0Cu, sb = 0x0Cu;
+        if (tnext[0] < N[0]) sa = tr[0].next();
+        if (tnext[1] < N[1]) sb = tr[1].next() + 4u;
+        ++tnext[0]; ++tnext[1];
+        return sa | 0x0C00u | (sb << 16) | 0x0C000000u;
+    };
+#pragma unroll
+    for (int j = 0; j < BMAX; ++j) {
+        int32_t v;
+        if (GOTOH) v = j == 0 ? 0 : (TYPE == NV_GLOBAL ? A.go + (j - 1) * A.ge : 0);
+        else v = TYPE == NV_GLOBAL ? j * A.del : 0;
+        H[j] = (uint32_t)(v + Bs) * 0x10001u;
+        F[j] = FLOOR;
+        sel[j] = 0x0C0C0C0Cu;
+    }
+#pragma unroll
+    for (int j = 0; j < BMAX - 1; ++j)
+        if ((uint32_t)j + 1 < Bn) sel[j] = next_sel();
+    // per-half sinks: taken at the half's last row (M == 0: from the row-zero band)
+    uint32_t out[2] = {0u, 0u};
+    bool have[2] = {false, false};
+    uint32_t best = FLOOR;
+    auto take = [&](int h) {
+        uint32_t v = 0;
+        if (TYPE == NV_GLOBAL) {
+#pragma unroll
+            for (int j = 0; j < BMAX; ++j)
+                if ((uint32_t)j + 1 == Bn) v = H[j];
+        } else if (TYPE == NV_SEMI) {
+            const uint32_t m = min(M[h] + Bn - 1, N[h]) - (M[h] - 1);   // uint32 as the reference
+            v = H[0];
+#pragma unroll
+            for (int j = 1; j < BMAX; ++j)
+                if ((uint32_t)j < Bn && (uint32_t)j < m) v = pk_max3(v, H[j], v);
+        } else {
+            v = best;
+        }
+        out[h] = v;
+        have[h] = true;
+    };
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+        if (M[h] == 0 && TYPE != NV_LOCAL) take(h);
+    const uint32_t Mmax = max(M[0], M[1]);
+    for (uint32_t i = 0; i < Mmax; ++i) {
+        // this row's tables: TA (low half, v_perm's second source), TB (high half, first source)
+        const uint32_t qa = i < M[0] ? prd[0].next() : 4u, qb = i < M[1] ? prd[1].next() : 4u;
+        const uint32_t TA = qa < 4 ? dm << (8 * qa) : 0u, TB = qb < 4 ? dm << (8 * qb) : 0u;
+        // the band's last slot reads text symbol i + B - 1
+        const uint32_t snew = next_sel();
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j)
+            if ((uint32_t)j + 1 == Bn) sel[j] = snew;
+        uint32_t E = 0, hprev = 0;
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j) {
+            if ((uint32_t)j >= Bn) break;
+            const bool last = (uint32_t)j + 1 == Bn;
+            const int jn = j + 1 < BMAX ? j + 1 : j;
+            const uint32_t tmp = H[j] + __builtin_amdgcn_perm(TB, TA, sel[j]) + MIS;   // H(i-1, i+j-1) + S
+            uint32_t hi;
+            if (GOTOH) {
+                F[j] = last ? NEG : pk_max3(F[jn] - GE, H[jn] - GO, FLOOR);
+                if (j == 0) hi = pk_max3(F[0], tmp, TYPE == NV_LOCAL ? BB : tmp);
+                else if (last) hi = pk_max3(E, tmp, TYPE == NV_LOCAL ? BB : tmp);
+                else hi = pk_max3(F[j], E, tmp);
+                E = j == 0 ? (TYPE == NV_LOCAL ? pk_max3(hi - GO, BB, BB) : hi - GO) : pk_max3(hi - GO, E - GE, FLOOR);
+            } else {
+                if (j == 0) hi = pk_max3(H[jn] - DEL, tmp, tmp);
+                else if (last) hi = pk_max3(hprev - INS, tmp, tmp);
+                else hi = pk_max3(H[jn] - DEL, hprev - INS, tmp);
+                if (TYPE == NV_LOCAL) hi = pk_max3(hi, BB, BB);
+            }
+            if (TYPE == NV_LOCAL) best = pk_max3(best, hi, best);
+            H[j] = hi;
+            hprev = hi;
+        }
+        // shift the selector window: row i + 1 reads text i + 1 + j
+#pragma unroll
+        for (int j = 0; j + 1 < BMAX; ++j)
+            if ((uint32_t)j + 1 < Bn) sel[j] = sel[j + 1];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (i + 1 == M[h]) take(h);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (!valid[h]) continue;
+        int32_t v = INT32_MIN;                                       // BestSink: nothing reported
+        if (N[h] >= M[h] && have[h]) v = (int32_t)((out[h] >> (16 * h)) & 0xFFFFu) - Bs;
+        A.score[2 * lane + h] = v;
+    }
+}
+
 }  // namespace gx

@@ -371,14 +371,15 @@ class Engine:
         return sc
 
     def nv_banded_score_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
-                                    scores_ptr: int, stream: int = 0):
+                                    scores_ptr: int, stream: int = 0, max_pattern_len: int = 0):
         """Device-resident banded scoring (gasalx_nv_banded_score_device); pat/txt as nv_score_device_ptrs."""
         mk = lambda d: CNvStrings(d["words"], d.get("offsets") or None, d.get("length", 0), d["bits"],
                                   int(d.get("big_endian", False)))
         ca = aligner.cstruct()
         _check(lib().gasalx_nv_banded_score_device(self._h, ctypes.byref(ca), ctypes.c_uint32(band), ctypes.c_uint32(n),
                                                    ctypes.byref(mk(pat)), ctypes.byref(mk(txt)),
-                                                   ctypes.c_void_p(scores_ptr or None), ctypes.c_void_p(stream or None)),
+                                                   ctypes.c_void_p(scores_ptr or None), ctypes.c_uint32(max_pattern_len),
+                                                   ctypes.c_void_p(stream or None)),
                "nv_banded_score_device")
 
     def nv_score_device_ptrs(self, aligner: "NvAligner", n: int, pat: dict, txt: dict, scores_ptr: int = 0,

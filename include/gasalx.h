@@ -259,12 +259,14 @@ int gasalx_nv_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, u
 
 /* nvbio's BatchedBandedAlignmentScore<band_len> (NvB/nvbio/alignment/batched.h:337,
  * batched_banded_inl.h:44-75): the banded DP of sw_banded_inl.h / gotoh_banded_inl.h /
- * ed_banded_inl.h over cells (i, i + j), 0 <= j < band_len (2..32), one pair per thread.
+ * ed_banded_inl.h over cells (i, i + j), 0 <= j < band_len (2..32): two pairs per lane in
+ * 16-bit halves for 2-bit texts inside the value window, else one pair per thread (int32).
  * BestSink score per pair; INT32_MIN when a text is shorter than its pattern (skipped,
  * as the reference does). */
 int gasalx_nv_banded_score_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band_len,
                                   uint32_t n_pairs, const gasalx_nv_strings *dev_patterns,
-                                  const gasalx_nv_strings *dev_texts, int32_t *dev_scores, void *stream);
+                                  const gasalx_nv_strings *dev_texts, int32_t *dev_scores,
+                                  uint32_t max_pattern_len, void *stream);   /* max_pattern_len: 0 = read back */
 int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band_len,
                                 uint32_t n_pairs, const gasalx_nv_strings *patterns, uint64_t pattern_words,
                                 const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores);

@@ -230,7 +230,7 @@ struct BatchedBandedAlignmentScore {
             exit(EXIT_FAILURE);
         }
         const int rc = gasalx_nv_banded_score_device(engine(), &a, BAND_LEN, stream.size(), &p, &t,
-                                                     stream.m_scores32, hip_stream);
+                                                     stream.m_scores32, stream.max_pattern_length(), hip_stream);
         if (rc != GASALX_OK) {
             fprintf(stderr, "BatchedBandedAlignmentScore::enact: %s\n", gasalx_last_error());
             exit(EXIT_FAILURE);

@@ -314,6 +314,34 @@ def test_banded_reference_known_answers(engine):
     assert int(engine.nv_banded_score_host(TN.ref_aligner(c), 7, P, T)[0]) == c["score"]
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 257, 4097])
+def test_banded_packed_equals_int32(engine, monkeypatch, n):
+    # the two-pairs-per-lane int16 kernel (2-bit texts) against the int32 one and the oracle:
+    # odd counts leave the last lane's high half empty; N pattern symbols, empty patterns,
+    # texts shorter than the pattern (skipped pairs) and patterns near the 16-bit window
+    rng = np.random.default_rng(900 + n)
+    pats, texts = [], []
+    for k in range(n):
+        m = int(rng.integers(0, 1200)) if k % 7 == 3 else int(rng.integers(0, 160))
+        t = list(rng.integers(0, 4, max(0, m + int(rng.integers(-4, 36)))))
+        p = _related(rng, t, m)
+        if k % 5 == 1 and m:
+            p[int(rng.integers(0, m))] = 4   # N
+        texts.append(np.array(t, np.uint32))
+        pats.append(np.array(p, np.uint32))
+    P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+    T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+    for base in ALIGNERS:
+        for type_ in (G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL):
+            for band in (3, 16, 29):
+                al = _al(base, type_)
+                g16 = _check_banded(engine, al, band, P, T)
+                monkeypatch.setenv("GASALX_NVB16", "0")
+                g32 = engine.nv_banded_score_host(al, band, P, T)
+                monkeypatch.delenv("GASALX_NVB16")
+                assert np.array_equal(g16, g32), (al, band)
+
+
 def test_banded_rejects_bad_band(engine):
     P = G.PackedSet.pack([np.zeros(4, np.uint32)])
     with pytest.raises(RuntimeError, match="band length"):
