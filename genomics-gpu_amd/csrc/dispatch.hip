@@ -1053,44 +1053,48 @@ static HmmFn hmm_lookup(int G) {
     }
 }
 
-// Two problems per lane group (pairhmm2_kernel): an A/B build only (-DGX_HMM2_BUILD=1,
-// then GASALX_HMM2=1 selects it).  Measured slower than one problem per group: 254
-// VGPRs hold it to 2 waves per SIMD (profiles/r03_pairhmm_ab.md).
-#ifndef GX_HMM2_BUILD
-#define GX_HMM2_BUILD 0
+// Two problems per lane group (pairhmm2_kernel) with kHmm2Rows read rows per lane: the
+// lane holds as many cells as pairhmm_kernel's (2 x 4 = 8), so its registers stay at three
+// waves per SIMD, while the eight cells of a column issue as four packed fp32 ops each.
+// The group is twice as wide for the same read (G = 64 for 250 rows): 31 more fill/drain
+// steps.  GASALX_HMM2=0 keeps the one-problem kernel (A/B).  With 8 rows per lane
+// (-DGX_HMM2_RR=8) the kernel needs 254 VGPRs, 2 waves, and is slower
+// (profiles/r03_pairhmm_ab.md).
+#ifndef GX_HMM2_RR
+#define GX_HMM2_RR 4
 #endif
+constexpr int kHmm2Rows = GX_HMM2_RR;
 template <bool QUALS, bool ABS>
 static HmmFn hmm2_lookup(int G) {
-#if !GX_HMM2_BUILD
-    (void)G;
-    return nullptr;
-#else
     switch (G) {
-        case 4: return &pairhmm2_kernel<4, kHmmRows, QUALS, ABS>;
-        case 8: return &pairhmm2_kernel<8, kHmmRows, QUALS, ABS>;
-        case 16: return &pairhmm2_kernel<16, kHmmRows, QUALS, ABS>;
-        case 32: return &pairhmm2_kernel<32, kHmmRows, QUALS, ABS>;
-        case 64: return &pairhmm2_kernel<64, kHmmRows, QUALS, ABS>;
+        case 4: return &pairhmm2_kernel<4, kHmm2Rows, QUALS, ABS>;
+        case 8: return &pairhmm2_kernel<8, kHmm2Rows, QUALS, ABS>;
+        case 16: return &pairhmm2_kernel<16, kHmm2Rows, QUALS, ABS>;
+        case 32: return &pairhmm2_kernel<32, kHmm2Rows, QUALS, ABS>;
+        case 64: return &pairhmm2_kernel<64, kHmm2Rows, QUALS, ABS>;
         default: return nullptr;
     }
-#endif
 }
 static bool hmm2_wanted() {
-    static const bool on = GX_HMM2_BUILD && env_flag("GASALX_HMM2", false);
+    static const bool on = env_flag("GASALX_HMM2", false);
     return on;
 }
 
-// lanes per pair for a read of max_r rows: kHmmRows (8) rows per lane, G in {4, ..., 64}
-int pairhmm_group(uint32_t max_r) {
+// lanes per pair for a read of max_r rows: `rows` read rows per lane, G in {4, ..., 64}
+static int hmm_group(uint32_t max_r, int rows) {
     for (int g : {4, 8, 16, 32, 64})
-        if ((uint32_t)g * kHmmRows >= max_r) return g;
+        if ((uint32_t)g * rows >= max_r) return g;
     return 0;
 }
+int pairhmm_group(uint32_t max_r) { return hmm_group(max_r, kHmmRows); }
 
 // One launch over slots [slot0, slot1) of A (A.perm maps slots to pairs, or NULL).
 static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0, uint32_t slot1, uint32_t max_h,
                           hipStream_t st) {
-    const int G = pairhmm_group(max_r);
+    // two problems per group where the read fits 64 x kHmm2Rows rows
+    const int per_group = hmm2_wanted() && hmm_group(max_r, kHmm2Rows) ? 2 : 1;
+    const int rows = per_group == 2 ? kHmm2Rows : kHmmRows;
+    const int G = hmm_group(max_r, rows);
     if (slot1 <= slot0) return GASALX_OK;
     if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
     A.slot0 = slot0;
@@ -1098,12 +1102,11 @@ static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0,
     A.lds_stride = (std::max<uint32_t>(max_h, 4) + 3) & ~3u;
     // reads shorter than the group's rows: the top lane's first row is virtual and
     // absorbs the boundary (pairhmm.hpp ABS)
-    const bool absorb = (uint32_t)G * kHmmRows > max_r;
+    const bool absorb = (uint32_t)G * rows > max_r;
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
-    // kHmmRows rows x 64 lanes x 4 bytes, per problem of a lane group
-    const int per_group = hmm2_wanted() ? 2 : 1;
+    // rows x 64 lanes x 4 bytes, per problem of a lane group
     const size_t lds = (((size_t)4 * per_group * (64 / G) * A.lds_stride + 15) & ~(size_t)15) +
-                       (size_t)per_group * 4 * 4 * kHmmRows * 64 * 4;
+                       (size_t)per_group * 4 * 4 * rows * 64 * 4;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
     HmmFn fn = per_group == 2 ? (quals ? (absorb ? hmm2_lookup<true, true>(G) : hmm2_lookup<true, false>(G))
                                        : (absorb ? hmm2_lookup<false, true>(G) : hmm2_lookup<false, false>(G)))

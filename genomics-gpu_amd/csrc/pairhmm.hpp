@@ -273,7 +273,7 @@ __device__ __forceinline__ hf2 shr_lane_fb2(hf2 v) { return hf2{shr_lane_fb(v.x)
 #define GX_HMM2_WAVES 2
 #endif
 template <int G, int RR, bool QUALS = false, bool ABS = false>
-__global__ __launch_bounds__(256, GX_HMM2_WAVES) void pairhmm2_kernel(HmmArgs A) {
+__global__ __launch_bounds__(256, RR <= 4 ? 3 : GX_HMM2_WAVES) void pairhmm2_kernel(HmmArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr int P = 64 / G;              // lane groups per wave, two problems each
     const float c0 = 1.329228e+36f, c09 = 0.9f, c01 = 0.1f;     // tile_1.cu:228-233
