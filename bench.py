@@ -59,10 +59,10 @@ WORKLOADS = {
                            bytes=340, ops=12,
                            label="config2 + WITH_START: SW local score+ends+starts, 1M pairs x 150bp per GPU"),
     "sw_local_tb": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL, start_pos=G.WITH_TB),
-                        bytes=340 + 152, ops=16,
+                        bytes=340 + 152, ops=16, streams=2,
                         label="config2 + WITH_TB: SW local score+ends+starts+CIGAR, 1M pairs x 150bp per GPU"),
     "nw_tb": dict(kind=3, pairs=100_000, scaling="weak", params=dict(algo=G.GLOBAL, start_pos=G.WITH_TB), bytes=650,
-                  ops=16, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
+                  ops=16, streams=2, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
     "semi": dict(kind=4, pairs=10_000_000, scaling="strong",
                  params=dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), bytes=364, ops=11,
                  label="config4: semi-global TARGET/TARGET, 10M 150bp reads in 182bp windows sharded over the "
@@ -116,6 +116,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="1-core CPU baseline sample budget")
     ap.add_argument("--parity-pairs", type=int, default=2_000_000,
                     help="per rank: check at most this many pairs of the shard against the oracle (0 = none)")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="GASAL workloads: engines (gasal_gpu_storage) on their own streams, steps "
+                         "issued round-robin as the reference's host program drives gasal_aln_async "
+                         "(test_prog.cpp NB_STREAMS = 2); 1 = every step on one stream.  Default: 2 for "
+                         "the traceback workloads (a step's walk runs beside the next step's DP), else 1")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave out the all-gather of scores")
@@ -594,6 +599,8 @@ def main():
 
     eng = G.Engine(dev_index)
     stream = torch.cuda.Stream(dev)      # a real (non-null) stream: kernels and timing events share it
+    # (engine, stream, gather) per set; GASAL workloads with --streams S > 1 hold S of them
+    sets, extra_bufs = [], []
     torch.cuda.set_stream(stream)
     gather = D.ScoreGather(counts, world, dev, dtype=torch.float32 if kind == 5 else torch.int32,
                            backend=backend) if do_gather else None
@@ -615,7 +622,7 @@ def main():
         plan = f"nvbanded16_gotoh_semi_B{band} (two pairs per lane, band in registers)" if band else \
             G.nv_describe_plan(al, rl, hl)
 
-        def align():
+        def align(k=0):
             if band:
                 eng.nv_banded_score_device_ptrs(al, band, n, pat, txt, result.data_ptr(), stream.cuda_stream, rl)
             else:
@@ -633,7 +640,7 @@ def main():
         hptrs = {k: v.data_ptr() for k, v in dh.items()}
         plan = f"pairhmm_wavefront (read {rl} x hap {hl})"
 
-        def align():
+        def align(k=0):
             eng.pairhmm_device_ptrs(hptrs, len(h["reads"]), len(h["haps"]), n, rl, hl, result.data_ptr(),
                                     stream.cuda_stream)
 
@@ -668,9 +675,25 @@ def main():
         plan = G.describe_plan(params, rl, hl)
         names = {"score": "aln_score", "q_end": "q_end", "t_end": "t_end", "q_start": "q_start",
                  "t_start": "t_start"}
+        # --streams S: S engines (own workspaces) on S streams, each with its own outputs
+        # (and, N > 1, its own exchange buffers); step i runs on set i % S, so a step's
+        # traceback walk runs beside the next step's DP.  Set 0's outputs (steps 0, S,
+        # 2S, ...) are the ones checked.
+        set_ptrs = [ptrs]
+        sets.append((eng, stream, gather))
+        inputs = ("q_batch", "t_batch", "q_offsets", "t_offsets", "q_lens", "t_lens", "seed_scores")
+        for _ in range(max(1, args.streams or wl.get("streams", 1)) - 1):
+            e2, s2 = G.Engine(dev_index), torch.cuda.Stream(dev)
+            g2 = D.ScoreGather(counts, world, dev, dtype=torch.int32, backend=backend) if gather else None
+            d2 = {k: (v if k in inputs else (g2.buf if g2 is not None and k == "aln_score" else torch.empty_like(v)))
+                  for k, v in d.items()}
+            sets.append((e2, s2, g2))
+            set_ptrs.append({k: v.data_ptr() for k, v in d2.items()})
+            extra_bufs.append(d2)
 
-        def align():
-            eng.align_device_ptrs(params, ptrs, batch.q_bytes, batch.t_bytes, n, rl, hl, stream.cuda_stream)
+        def align(k=0):
+            sets[k][0].align_device_ptrs(params, set_ptrs[k], batch.q_bytes, batch.t_bytes, n, rl, hl,
+                                         sets[k][1].cuda_stream)
 
         def results():
             r = {f: d[names[f]][:n].cpu().numpy() for f in fields}
@@ -680,14 +703,19 @@ def main():
             return r
     torch.cuda.synchronize(dev)
     synth_s = time.perf_counter() - t_syn
+    if not sets:
+        sets.append((eng, stream, gather))
+    n_sets = len(sets)
 
-    def step():
-        align()
-        if gather is not None:       # the exchange step of SURVEY §8(e): every rank gets all scores
-            gather()
+    def step(i):
+        k = i % n_sets
+        align(k)
+        if sets[k][2] is not None:   # the exchange step of SURVEY §8(e): every rank gets all scores
+            with torch.cuda.stream(sets[k][1]):
+                sets[k][2]()
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -695,23 +723,32 @@ def main():
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        ev[i][0].record(stream)
-        align()
-        ev[i][1].record(stream)
-        if gather is not None:
-            gather()
-        ev[i][2].record(stream)
+        k = (args.warmup + i) % n_sets
+        st_i, g_i = sets[k][1], sets[k][2]
+        ev[i][0].record(st_i)
+        align(k)
+        ev[i][1].record(st_i)
+        if g_i is not None:
+            with torch.cuda.stream(st_i):
+                g_i()
+        ev[i][2].record(st_i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    ev_ms = kern_ms
     gath_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     t = torch.tensor([elapsed, kern_ms, gath_ms], dtype=torch.float64, device=dev)
     if world > 1:
         t = allreduce(t, dist.ReduceOp.MAX)
     elapsed, kern_ms, gath_ms = (float(x) for x in t)
+    if n_sets > 1:
+        # launches of consecutive steps overlap on the two streams: a launch's own duration
+        # (events, rocprof) includes the time it shares the GPU, so the kernel time of a step
+        # is its share of the wall time
+        kern_ms = elapsed * 1e3 / args.steps
 
     # ---- parity: this rank's shard against the oracle (the CPU baseline at N = 1) ----
     parity, cpu = None, None
@@ -882,12 +919,18 @@ def main():
                                         ", gloo all-gather of scores (through host memory) in every step")
                                        if gather else ""),
                        **({"dist_backend": backend, "devices": n_dev} if world > 1 else {}),
+                       **({"streams": f"{n_sets} engines on {n_sets} streams, steps round-robin "
+                                      f"(gasal_aln_async per storage, test_prog.cpp's NB_STREAMS)"}
+                          if n_sets > 1 else {}),
                        "synth_s_rank0": round(synth_s, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "bytes_per_pair": wl["bytes"], "kernel_ms": round(kern_ms, 4),
-                         "timed": "HIP events around the align call on its stream (every kernel of the call; "
-                                  "WITH_START/WITH_TB calls launch more than the dominant kernel)"},
+                         "timed": ("HIP events around the align call on its stream (every kernel of the call; "
+                                   "WITH_START/WITH_TB calls launch more than the dominant kernel)") if n_sets == 1 else
+                                  (f"wall time per step of the {n_sets}-stream round-robin (steps overlap; "
+                                   f"HIP events around one align call on its stream: {ev_ms:.4f} ms, the "
+                                   f"launches sharing the GPU with the other stream's)")},
             "valu_roofline": valu,
             "kernel_gcups": round(cells_per_step / kern_s / 1e9, 2),
             "gather_ms": round(gath_ms, 4) if gather else None,
