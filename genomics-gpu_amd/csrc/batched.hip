@@ -206,6 +206,12 @@ namespace {
 using NvBandFn = void (*)(NvBandArgs);
 template <int ALN, int TYPE>
 NvBandFn nv_band_pick(uint32_t band) {
+    switch (band) {
+        case 8: return &nv_banded_kernel<ALN, TYPE, 8, true>;
+        case 16: return &nv_banded_kernel<ALN, TYPE, 16, true>;
+        case 32: return &nv_banded_kernel<ALN, TYPE, 32, true>;
+        default: break;
+    }
     if (band <= 8) return &nv_banded_kernel<ALN, TYPE, 8>;
     if (band <= 16) return &nv_banded_kernel<ALN, TYPE, 16>;
     if (band <= 32) return &nv_banded_kernel<ALN, TYPE, 32>;
@@ -219,6 +225,12 @@ NvBandFn nv_band_lookup_t(int type, uint32_t band) {
 using NvBand16Fn = void (*)(NvBand16Args);
 template <int ALN, int TYPE>
 NvBand16Fn nv_band16_pick(uint32_t band) {
+    switch (band) {   // band lengths of an instance's own size: the slot tests fold
+        case 8: return &nv_banded16_kernel<ALN, TYPE, 8, true>;
+        case 16: return &nv_banded16_kernel<ALN, TYPE, 16, true>;
+        case 32: return &nv_banded16_kernel<ALN, TYPE, 32, true>;
+        default: break;
+    }
     if (band <= 8) return &nv_banded16_kernel<ALN, TYPE, 8>;
     if (band <= 16) return &nv_banded16_kernel<ALN, TYPE, 16>;
     if (band <= 32) return &nv_banded16_kernel<ALN, TYPE, 32>;

@@ -61,7 +61,7 @@ struct NvSymReader {
     }
 };
 
-template <int ALN, int TYPE, int BMAX>
+template <int ALN, int TYPE, int BMAX, bool EX = false>   // EX: band length == BMAX (as nv_banded16_kernel)
 __global__ __launch_bounds__(256) void nv_banded_kernel(NvBandArgs A) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= A.n) return;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void nv_banded_kernel(NvBandArgs A) {
     const bool shared = A.toff == nullptr;
     const uint32_t to = shared ? 0u : A.toff[tid], N = shared ? A.tlen0 : A.toff[tid + 1] - to;
     int32_t best = INT32_MIN;                              // BestSink (sink_inl.h:38-40, 59-68)
-    const uint32_t B = A.band;
+    const uint32_t B = EX ? (uint32_t)BMAX : A.band;
     if (N < M) { A.score[tid] = best; return; }            // gotoh_banded_inl.h:424, sw_banded_inl.h:365
     constexpr bool GOTOH = ALN == NV_GOTOH;
     const int32_t S_eq = A.match, S_ne = A.mismatch;
@@ -164,7 +164,9 @@ struct NvBand16Args {
     uint32_t base;                  // stored value of 0
 };
 
-template <int ALN, int TYPE, int BMAX>
+// EX: the band length is BMAX itself (nvbio's BAND_LEN is a template argument; 8, 16 and
+// 32 get their own code), so the band-slot tests fold at compile time
+template <int ALN, int TYPE, int BMAX, bool EX = false>
 __global__ __launch_bounds__(256) void nv_banded16_kernel(NvBand16Args A) {
     const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
     if (lane >= A.n_lanes) return;
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(256) void nv_banded16_kernel(NvBand16Args A) {
         to[h] = shared ? 0u : A.toff[pp];
         N[h] = shared ? A.tlen0 : A.toff[pp + 1] - to[h];
     }
-    const uint32_t Bn = A.band;
+    const uint32_t Bn = EX ? (uint32_t)BMAX : A.band;
     const int32_t Bs = (int32_t)A.base;
     const uint32_t BB = A.base * 0x10001u, NEG = 0x04000400u;
     const uint32_t FLOOR = TYPE == NV_LOCAL ? BB : NEG;
