@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 3: the whole GPU test suite at the current tree, then smoke.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/r03y
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc $(tail -1 $O/pytest.log)"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc $(tail -1 $O/smoke.log)"; exit $rc
