@@ -5,6 +5,6 @@
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 for w in "$@"; do
-  bash "$ROOT/scripts/pmc_session.sh" "$w" --workload "$w" --parity-pairs 0 --no-e2e || exit $?
+  bash "$ROOT/scripts/pmc_session.sh" "$w" --workload "$w" --parity-pairs 0 --no-e2e --streams 1 || exit $?
 done
 exit 0
