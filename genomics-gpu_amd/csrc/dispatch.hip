@@ -149,11 +149,17 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
         const bool tq = p.start_pos == 0 && (p.tail == 1 || p.tail == 3);
         if (p.tail != 2 && !tq) return false;
         if (tq && (t8 > 256 || q8 > 65535)) return false;
-        if (oe < b || oe < npen) return false;                 // table offset K = OE
-        k = oe;
+        // table offset K = OE + e (wavefront16.hpp step_semi's frame): bytes s + K >= 0
+        if (oe + e < b || oe + e < npen) return false;
+        k = oe + e;
     } else {
-        drift = (std::max(b, npen) + 1) / 2;                   // GLOBAL: values drift by D per anti-diagonal,
-        k = 2 * drift;                                         // table offset K = 2D (pk16_params)
+        // GLOBAL: values drift by e per anti-diagonal, table offset K = max(2*ceil(max(b,
+        // npen)/2), 2e) (pk16_params, step_global).  Traceback reads the first pad query
+        // row, scored -K: keep the round-2 offset there (K == 2*ceil(max(b, npen)/2))
+        drift = e;
+        const int64_t k0 = 2 * ((std::max(b, npen) + 1) / 2);
+        k = std::max(k0, 2 * e);
+        if (p.start_pos == 2 && k != k0) return false;
     }
     if (a + k > 255) return false;
     // span: largest row + column of any cell the launch computes.  Both halves of
@@ -164,8 +170,19 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
     // no floor on E/F; values fall by at most e per row or column along a gap).
     // make_plan checks again with the chosen shape's span.
     if (!span) span = q8 + t8 + 2 * 64 + 8;
-    const int64_t v = 4 * oe + k + e * span + 2 * drift + 64;   // below every reachable value
     const int64_t neg = 0x400 + 2 * e + 16;
+    if (wf_algo == WF_SEMI) {
+        // SEMI's frame (+ e per anti-diagonal): E and F never decay, every F is at least
+        // its column's top boundary and every E its row's left one, so no value falls
+        // below B - 3*OE whatever the span; values rise by the frame, e per row + column
+        // (the tail keys add up to e*(span) more to put the last row or column in one frame)
+        const int64_t v = 4 * oe + k + 64;
+        top = neg + v + a * std::min(q8, t8) + a + k + oe + 64 + e * (2 * span + 1);
+        if (top > 0x7BFF) return false;
+        *vmin = (int32_t)v;
+        return true;
+    }
+    const int64_t v = 4 * oe + k + e * span + 2 * drift + 64;   // below every reachable value
     top = neg + v + a * std::min(q8, t8) + a + k + oe + 64 + drift * span;
     if (top > 0x7BFF) return false;
     *vmin = (int32_t)v;

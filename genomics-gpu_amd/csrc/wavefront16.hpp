@@ -39,9 +39,10 @@
 //   GLOBAL (global.h:4-12; the NEG floors never bind for reachable values):
 //     same without the key and with NEG in place of B: 9 instructions.
 //   SEMI   (semiglobal_kernel_template.h:17-28, H-based Gotoh; values stored
-//           as H - OE and the table offset K = OE folds the + OE):
-//     tmp = diag + v; F = max(Hup, F - e); E = max(Hleft, E - e);
-//     H' = max3(tmp, F, E) - OE: 8 instructions.
+//           as H - OE, every value drifting by e per anti-diagonal, so that the
+//           gap extensions vanish and the table offset K = OE + e folds the + OE):
+//     tmp = diag + v; F = max(Hup, F); E = max(Hleft, E);
+//     H' = max3(tmp, F, E) - o: 6 instructions (8 before the drift).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -124,11 +125,11 @@ __device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
         P.neg = P.base;
         P.drift = 0;
     } else {
-        P.k = (ALGO == WF_SEMI) ? OE : max(A.b, A.has_npen ? A.npen : 0);
+        P.k = (ALGO == WF_SEMI) ? OE + A.e : max(A.b, A.has_npen ? A.npen : 0);   // SEMI: step_semi's frame
         P.drift = 0;
-        if (ALGO == WF_GLOBAL) {       // table offset 2*drift: diag + byte is tmp itself
-            P.drift = (P.k + 1) >> 1;
-            P.k = 2 * P.drift;
+        if (ALGO == WF_GLOBAL) {       // drift e, table offset K >= 2e (step_global)
+            P.drift = A.e;
+            P.k = max(2 * ((P.k + 1) >> 1), 2 * A.e);
         }
         P.neg = 0x0400 + 2 * A.e + 16;
         P.base = P.neg + A.vmin;
@@ -177,24 +178,28 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
 // ---------------------------------------------------------------------------
 // GLOBAL step: as LOCAL without the floor at 0 and without keys.
 // ---------------------------------------------------------------------------
-// Values drift: cell (r, c) is stored as value + B + D*(r+c) with table offset
-// K = 2D, so diag + byte is tmp itself (no subtraction), and E and F, which move
-// one anti-diagonal, take toe = tmp - (OE - D) and an extend of e - D (32-bit
-// adds/subtracts of a signed per-half constant, exact either way round).
+// Values drift by the gap extension: cell (r, c) is stored as value + B + e*(r+c)
+// (D = e), so E and F, which move one anti-diagonal and fall by e per step, stay
+// put: E' = max3(toe, E, NEG) with toe = tmp - OE + e, no extension subtract.  The
+// diagonal gains 2e: with table offset K (bytes s + K >= 0) tmp = diag + v - KX,
+// KX = K - 2e >= 0 (K = max(2*ceil(max(b, npen)/2), 2e)); toe = diag + v - (KX +
+// OE - e).  7 instructions per two cells (8 with the round-2 drift K/2, which
+// left an extension add).  32-bit adds/subtracts of per-half constants, exact.
 template <int R>
 __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                             const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
-                                            uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t OED,
-                                            const uint32_t EXT, const uint32_t NN) {
+                                            uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t KX,
+                                            const uint32_t OEX, const uint32_t NN) {
     uint32_t diag = diag_top, f = f_top;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
-        const uint32_t tmp = pk_addnc(diag, v);
-        const uint32_t toe = pk_subnb(tmp, OED);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KX);
+        const uint32_t toe = pk_subnb(t1, OEX);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
-        Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), NN);
-        f = pk_max3(toe, pk_subnb(f, EXT), NN);
+        Ek[k] = pk_max3(toe, Ek[k], NN);
+        f = pk_max3(toe, f, NN);
         diag = Hin[k];
         Hout[k] = H;
     }
@@ -235,17 +240,18 @@ template <int R>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                                uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
-                                               uint32_t &f_out, const uint32_t OED, const uint32_t EXT,
+                                               uint32_t &f_out, const uint32_t KX, const uint32_t OEX,
                                                const uint32_t NN, const int j) {
     const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
     uint32_t diag = diag_top, f = f_top, tx = T.x, ty = T.y;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(ty, tx, xs[k]);
-        const uint32_t tmp = pk_addnc(diag, v);          // drift: see step_global
-        const uint32_t toe = pk_subnb(tmp, OED);
+        const uint32_t t1 = pk_addnc(diag, v);           // drift e: see step_global
+        const uint32_t tmp = pk_subnb(t1, KX);
+        const uint32_t toe = pk_subnb(t1, OEX);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
-        const uint32_t em = pk_subnb(Ek[k], EXT), fm = pk_subnb(f, EXT);
+        const uint32_t em = Ek[k], fm = f;               // E - e and F - e, in the frame
         const uint32_t En = pk_max3(toe, em, NN);
         const uint32_t Fn = pk_max3(toe, fm, NN);
         const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, em), fy = tb_flag(toe, fm);
@@ -308,26 +314,30 @@ __device__ __forceinline__ void step_local_tb(const uint2 T, const int32_t c, co
 
 // ---------------------------------------------------------------------------
 // SEMI step (transposed): registers = target columns, one query row per step.
-// Stored values are H - OE ("Hm").  In: diag_top = Hm(r-1, c0-1),
-// hl/el = Hm(r, c0-1) / E(r, c0-1) entering the lane's first column.
+// Values drift by e per anti-diagonal (semi_frame below): cell (r, c) stores
+//   F^ = B + F + e(r+c),  E^ = B + E + e(r+c),  Hm^ = B + H - OE + e(r+c) + e,
+// so the gap extensions cost nothing, F(r,c) = max(Hm(r-1,c), F(r-1,c) - e) is
+// max(Hm^(r-1,c), F^(r-1,c)) and E likewise, the diagonal H(r-1,c-1) + s is
+// Hm^(r-1,c-1) + (s + OE + e) (table offset K = OE + e) and Hm^ = max3 - o:
+// 6 instructions per two cells instead of 8.  In: diag_top = Hm^(r-1, c0-1),
+// hl/el = Hm^(r, c0-1) / E^(r, c0-1) entering the lane's first column.
 // ---------------------------------------------------------------------------
 // PV > 0 (TAIL=QUERY/BOTH kernel): the last PV registers may hold pad columns of the
 // target, which the reference scores by its N rule (Q6/Q7, read by Q11); their selector
-// picks the constant 0 and pv adds the N score + OE per half (0 for real columns).
+// picks the constant 0 and pv adds the N score + K per half (0 for real columns).
 template <int R, int PV = 0>
 __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top, uint32_t &hl, uint32_t &el,
                                           const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
-                                          uint32_t (&Fk)[R], const uint32_t OE, const uint32_t EXT,
-                                          const uint32_t *pv = nullptr) {
+                                          uint32_t (&Fk)[R], const uint32_t GO, const uint32_t *pv = nullptr) {
     uint32_t diag = diag_top, h = hl, e = el;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
         if (PV > 0 && k >= R - PV) v = pk_addnc(v, pv[k - (R - PV)]);
         const uint32_t tmp = pk_addnc(diag, v);                     // H(r-1,c-1) + s
-        Fk[k] = pk_max_u16(Hin[k], pk_subnb(Fk[k], EXT));            // F(r,c)
-        e = pk_max_u16(h, pk_subnb(e, EXT));                         // E(r,c)
-        h = pk_subnb(pk_max3(tmp, Fk[k], e), OE);                    // H(r,c) - OE
+        Fk[k] = pk_max_u16(Hin[k], Fk[k]);                           // F(r,c)
+        e = pk_max_u16(h, e);                                        // E(r,c)
+        h = pk_subnb(pk_max3(tmp, Fk[k], e), GO);                    // H(r,c) - OE
         diag = Hin[k];
         Hout[k] = h;
     }
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             pv[j] = 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if (valid[h] && r >= xl[h] && r < xpad[h]) pv[j] |= (uint32_t)(nrule + A.o + A.e) << (16 * h);
+                if (valid[h] && r >= xl[h] && r < xpad[h]) pv[j] |= (uint32_t)(nrule + P.k) << (16 * h);
         }
 #pragma unroll
         for (int h = 0; h < 2; ++h) other |= valid[h] && xpad[h] != (uint32_t)(G * R);   // the launch's class
@@ -527,8 +537,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 
     const uint32_t nsteps = ymaxw + G - 1;
     const uint2 *tcol = wl + slot * words;
-    const uint32_t OE = pk_bcast(A.o + A.e);
     const uint32_t EXT = pk_bcast(A.e);
+    const uint32_t GO = pk_bcast(A.o);                   // SEMI: Hm^ = max3 - o (step_semi's frame)
     const uint32_t BB = (uint32_t)P.base * 0x10001u;
     const uint32_t NN = (uint32_t)P.neg * 0x10001u;
     const bool top = lg == 0;
@@ -639,9 +649,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // boundaries (global.h:57-71, Q2): H(r,-1) = -(o+e*r) (0 for r = 0), E = -inf;
         // top: H(-1,c-1) = -(o+e*c) (0 for c = 0), F = -inf.  Lanes sweep garbage
         // columns c < -1 first and reset to the left boundary at c = -1.
-        const int32_t pb = P.base, go = A.o, ge = A.e, D = P.drift;
-        // signed per-half constants: a 32-bit subtract of c*0x10001 is exact per half for either sign
-        const uint32_t OED = (uint32_t)((A.o + A.e - D) * 0x10001), EXTD = (uint32_t)((A.e - D) * 0x10001);
+        const int32_t pb = P.base, go = A.o, ge = A.e, D = P.drift;   // D = e (step_global)
+        const uint32_t KX = pk_bcast(P.k - 2 * D), OEX = pk_bcast(P.k - 2 * D + A.o + A.e - D);
         // H(r, -1) (Q2), stored at anti-diagonal r - 1
         auto left = [=](int32_t r) -> uint32_t {
             return (uint32_t)(pb + D * (r - 1) - (r <= 0 ? 0 : go + ge * r)) * 0x10001u;
@@ -688,10 +697,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // H(-1, c-1) at anti-diagonal c - 2
                 const uint32_t dtop = (uint32_t)(pb + D * (cc - 2) - (cc <= 0 ? 0 : go + ge * cc)) * 0x10001u;
                 if constexpr (GTB)
-                    step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, OED,
-                                      EXTD, NN, j);
+                    step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, KX,
+                                      OEX, NN, j);
                 else
-                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, OED, EXTD, NN);
+                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KX, OEX, NN);
 #if GX_WF16_CAPTURE_TREE
                 // branch-free capture: every lane picks one register by a select tree
                 // over the bits of its index (score: row xl - 1 at column yl - 1; fix:
@@ -822,13 +831,19 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         //   top   diag into (0,c): head_t ? 0 : -(o+e*c) (0 for c = 0)                         (:127)
         //         F(0,c) = hu(c) - OE, hu(c) = head_t ? 0 : -(o+e*c)                           (:125, Q3)
         // Lanes sweep garbage rows r < -1 first and reset to row -1 at r = -1.
+        // Every value is stored in step_semi's frame (+ e per anti-diagonal, Hm^ one e
+        // more): Hm^(r, c) = B + H - OE + e(r + c + 1); reads subtract it again.
         const bool head_q = (A.head == 1 || A.head == 3), head_t = (A.head == 2 || A.head == 3);
         const int32_t oe = A.o + A.e, pb = P.base, go = A.o, ge = A.e;
-        auto hm = [=](int32_t val) -> uint32_t { return (uint32_t)(pb + val - oe) * 0x10001u; };   // H - OE
-        auto hleft = [=](int32_t r) -> uint32_t {      // Hm(r, -1); r = -1 gives H(-1,-1) = 0
-            return (uint32_t)(pb - oe + (head_q ? 0 : (r <= 0 ? 0 : -(go + ge * r)))) * 0x10001u;
+        auto hm = [=](int32_t val, int32_t r, int32_t c) -> uint32_t {   // Hm^ of H value val at (r, c)
+            return (uint32_t)(pb + val - oe + ge * (r + c + 1)) * 0x10001u;
         };
-        const uint32_t eleft = head_q ? BB : NN;        // E(r,-1)
+        auto hleft = [=](int32_t r) -> uint32_t {      // Hm^(r, -1); r = -1 gives H(-1,-1) = 0
+            return (uint32_t)(pb - oe + (head_q ? 0 : (r <= 0 ? 0 : -(go + ge * r))) + ge * r) * 0x10001u;
+        };
+        // E^(r, -1): 0 (HEAD=QUERY/BOTH) at frame e(r - 1), else -inf (NN is below every
+        // value the frame can hold and, undecayed, stays there)
+        auto eleft = [=](int32_t r) -> uint32_t { return head_q ? (uint32_t)(pb + ge * (r - 1)) * 0x10001u : NN; };
         uint32_t HA[R], HB[R], Fk[R];
         auto reset = [&](uint32_t (&H)[R]) {
             // computed where used: hoisting 2R loop-invariant values out of the sweep would spill
@@ -839,8 +854,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 const int32_t col = c0 + k;
                 const int32_t hd = head_t ? 0 : -(go + ge * (col + 1));   // H(-1,col) as diag of (0,col+1)
                 const int32_t hu = head_t ? 0 : -(go + ge * col);         // H(-1,col) as F source (Q3)
-                H[k] = hm(hd);
-                Fk[k] = (uint32_t)(pb + hu - oe + ge) * 0x10001u;         // F(0,col) = hu - OE exactly
+                H[k] = hm(hd, -1, col);
+                Fk[k] = (uint32_t)(pb + hu - oe + ge * col) * 0x10001u;   // F^(0,col) = hu - OE exactly (>= H[k])
             }
         };
         reset(HA);
@@ -856,7 +871,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         if (A.stop) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if (valid[h]) thrp[h] = A.stop[pr[h]] + pb - oe;   // stored pattern of the forward score
+                if (valid[h]) thrp[h] = A.stop[pr[h]] + pb - oe + ge * (int32_t)(yl[h] + G * R);   // its key-frame pattern
         }
         // Lane lg's first real step (row 0, column r0) takes its diagonal from the
         // upper lane's reset at row -1, i.e. H(-1, r0 - 1).  Lanes lg >= 2 receive it
@@ -864,7 +879,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // reset step, so the value is seeded here.  Seeding it with the lane's own
         // H(-1, r0 + R - 1) made cell (0, R) of lane 1 wrong with HEAD=NONE, which
         // surfaced on few-row shapes (the diagonal entry at column R is cheap there).
-        const uint32_t hd_up = hm(head_t ? 0 : (r0 == 0 ? 0 : -(go + ge * (int32_t)r0)));
+        const uint32_t hd_up = hm(head_t ? 0 : (r0 == 0 ? 0 : -(go + ge * (int32_t)r0)), -1, (int32_t)r0 - 1);
         uint32_t recvH = hd_up, prevRecvH = hd_up, recvE = NN, hl = 0, el = 0;
         uint2 tnext = tcol[c + G];
         auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
@@ -874,15 +889,17 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 reset(Hout);
             } else {
                 hl = top ? hleft(cc) : recvH;
-                el = top ? eleft : recvE;
-                step_semi<R, PV>(T, top ? hleft(cc - 1) : prevRecvH, hl, el, xs, Hin, Hout, Fk, OE, EXT, pv);
+                el = top ? eleft(cc) : recvE;
+                step_semi<R, PV>(T, top ? hleft(cc - 1) : prevRecvH, hl, el, xs, Hin, Hout, Fk, GO, pv);
                 if constexpr (TQ) {
                     // semiglobal :185-193 (Q11): H of row cc at the last padded column, which is
                     // register R - 1 of lane G - 1 (the other lanes' keys are never read);
                     // the largest key is the first row of the maximum
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const uint32_t v = (Hout[R - 1] >> (16 * h)) & 0xFFFFu;
+                        // rows compared in one frame: cell (cc, G*R - 1) + e*(yl - cc), which is
+                        // the old-frame pattern + e*(yl + G*R) and positive for cc < yl
+                        const uint32_t v = ((Hout[R - 1] >> (16 * h)) & 0xFFFFu) + (uint32_t)ge * (yl[h] - (uint32_t)cc);
                         const uint32_t cand = (uint32_t)cc < yl[h] ? (v << 16) | (0xFFFFu - (uint32_t)cc) : 0u;
                         bestq[h] = cand > bestq[h] ? cand : bestq[h];
                     }
@@ -893,7 +910,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                         for (int k = 0; k < R; ++k) {
                             const uint32_t col = r0 + k;
-                            const uint32_t v = (Hout[k] >> (16 * h)) & 0xFFFFu;
+                            // columns compared in one frame: cell (yl - 1, col) + e*(G*R - col),
+                            // the old-frame pattern + e*(yl + G*R) (thrp too); positive
+                            const uint32_t v = ((Hout[k] >> (16 * h)) & 0xFFFFu) + (uint32_t)ge * ((uint32_t)(G * R) - col);
                             const uint32_t cand =
                                 col >= xl[h] ? 0u
                                 : (int32_t)v >= thrp[h]
@@ -920,18 +939,20 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             const uint32_t bq = TQ ? (uint32_t)__shfl(bestq[h], (int)(slot * G + G - 1)) : 0u;
             if (valid[h] && lg == 0) {
                 // semiglobal :49,63-64,206-218 (Q10): q_end = tl, t_end = column of the max
+                // keys hold the old-frame pattern + e*(yl + G*R) (see the captures)
+                const int32_t kof = pb - oe + ge * (int32_t)(yl[h] + G * R);
                 int32_t score = -32768, qe = (int32_t)xl[h], te = (int32_t)yl[h];
                 if (b & 0x80000000u) {
-                    score = (int32_t)((b >> 8) & 0x7FFFu) - pb + oe;
+                    score = (int32_t)((b >> 8) & 0x7FFFu) - kof;
                     te = (int32_t)(8 * (255u - ((b >> 23) & 255u)) + (255u - (b & 255u)));
                 } else if (b != 0) {
-                    score = (int32_t)(b >> 16) - pb + oe;
+                    score = (int32_t)(b >> 16) - kof;
                     te = (int32_t)(0xFFFFu - (b & 0xFFFFu));
                 }
                 if (TQ && bq != 0) {
                     // :185-203: a row of the last padded column strictly above the maximum so
                     // far moves the end to (row, ...); then t_end = ql unless that row is tl
-                    const int32_t vq = (int32_t)(bq >> 16) - pb + oe;
+                    const int32_t vq = (int32_t)(bq >> 16) - kof;
                     if (vq > score) { score = vq; qe = (int32_t)(0xFFFFu - (bq & 0xFFFFu)); }
                 }
                 if (TQ && qe != (int32_t)xl[h]) te = (int32_t)yl[h];
