@@ -74,6 +74,18 @@ bool nv16_ok(int aligner, int type, int32_t match, int32_t mismatch, int32_t go,
                                            std::abs((int64_t)ge), std::abs((int64_t)del), std::abs((int64_t)ins), 1});
     if (mag > 0x200) return false;   // a gap subtracted from NEG must not borrow across the halves
     const int64_t vabs = ((int64_t)max_p + max_t + 2) * mag * 2;
+    if (aligner == NV_GOTOH && type != NV_LOCAL) {
+        // the drift frame (nvbio16.hpp FR): values + g*(r+c) + (go - ge) lie within the
+        // all-gap path below and the diagonal above; virtual rows (r >= -G*R, G*R <=
+        // 2*max_p + 64) fall by g per row, sink keys add up to g*max_t
+        const int64_t g = -(int64_t)ge, gr = 2 * (int64_t)max_p + 64;
+        const int64_t b = 0x400 + g * (gr + 2) + 4 * (std::abs((int64_t)go) + g) + 64;
+        const int64_t top = b + std::abs((int64_t)go - ge) + std::max<int64_t>(match, 0) * max_p +
+                            g * ((int64_t)max_p + 2 * (int64_t)max_t + 4) + 512;
+        if (top > 0x7BFF) return false;
+        *base = (uint32_t)b;
+        return true;
+    }
     const int64_t b = 0x400 + 2 * (std::abs((int64_t)go) + std::abs((int64_t)ge) + std::abs((int64_t)del) +
                                    std::abs((int64_t)ins)) + vabs + 64;
     if (b + vabs + 512 > 0x7BFF) return false;

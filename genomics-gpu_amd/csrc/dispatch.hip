@@ -319,6 +319,13 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin,
                                           (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8);
             pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
+            // LOCAL score kernels: keys 0x0400 + H*C + (C-1-c) with C = the padded target
+            // length fit the f16 window when (Hmax + 1) * C <= 0x7800 (step_local KU);
+            // GASALX_KF16=0 keeps the 16-bit keys (A/B runs)
+            if (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && env_flag("GASALX_KF16", true)) {
+                const int64_t hmax = (int64_t)std::max(p.match, 0) * std::min(q8, t8);
+                if ((hmax + 1) * (int64_t)y8 <= 0x7800) pl.kf16 = y8;
+            }
             pl.semi_tq = pl.semi_tq && pl.packed16;
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
@@ -381,6 +388,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         P16.lds_stride = pl.lds16_stride;
         P16.fast16 = 1;
         P16.vmin = pl.vmin;
+        P16.kf16 = pl.kf16;
         const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
         const uint32_t grid16 = grid_for(n, ppb16);
         HIPCHK(ws.misc.reserve(grid16 + 64));

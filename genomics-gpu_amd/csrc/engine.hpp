@@ -56,6 +56,7 @@ struct Plan {
     uint32_t lds16_stride = 0;
     size_t lds16_bytes = 0;
     int32_t vmin = 0;       // packed GLOBAL/SEMI value-range bound
+    uint32_t kf16 = 0;      // packed LOCAL: f16-pattern key columns (wavefront16.hpp step_local KU), 0 = 16-bit keys
     int G = 0, R = 0;
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;

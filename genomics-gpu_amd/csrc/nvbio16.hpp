@@ -21,6 +21,13 @@
 // mismatch is one v_add3.  Per cell of both pairs, Gotoh: v_perm, v_add3, F
 // (2 sub + maximum3), E (2 sub + maximum3), H (maximum3): 9 instructions.
 //
+// Gotoh SEMI_GLOBAL / GLOBAL (FR): values drift by g = -ge per anti-diagonal, as in
+// wavefront16.hpp's SEMI frame: F^ = B + F + g(r+c), E^ likewise, H^ = B + H + g(r+c)
+// + (go - ge), so F(r,c) = max(F(r-1,c) + ge, H(r-1,c) + go) is max(F^up, H^up), E
+// likewise, tmp^ = H^dg + byte + (mismatch + g - go) and H^ = max3 + (go - ge): 6
+// instructions per cell of both pairs instead of 9.  Sinks compare a row's columns
+// in one frame (+ g*(N-1-c)); the outputs take the frame off again.
+//
 // Sinks (sink_inl.h:59-68): LOCAL every cell (a running maximum3 over two cells
 // per instruction; pad rows and columns score <= 0 and never exceed a real cell,
 // which the host requires); SEMI_GLOBAL row M-1 of each pair at every column;
@@ -58,6 +65,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     extern __shared__ __attribute__((aligned(16))) uint32_t nvt[];
     constexpr int P = 64 / G;
     constexpr bool GOTOH = ALN == NV_GOTOH;
+    constexpr bool FR = GOTOH && TYPE != NV_LOCAL;   // the drift frame (header)
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1), grp = lane / G;
     const uint32_t pa = 2 * ((blockIdx.x * 4 + wave) * P + grp), pb = pa + 1;
@@ -117,6 +125,9 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
         return GOTOH ? A.go + A.ge * r : A.ins * (r + 1);
     };
     auto pk2 = [&](int32_t a, int32_t b) { return (uint32_t)(a + B) | ((uint32_t)(b + B) << 16); };
+    const int32_t g = -A.ge, dl = A.go - A.ge;           // FR: drift per anti-diagonal, H^ offset
+    // FR: H^ of H value h at (r, c)
+    auto fr = [&](int32_t h, int32_t r, int32_t c) { return h + g * (r + c) + dl; };
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const int32_t ra = ra0 + k, rb = rb0 + k;
@@ -127,7 +138,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
         const uint32_t sa = ra < 0 ? 4u : (ca < 4 ? ca : 0x0Cu);
         const uint32_t sb = rb < 0 ? 4u : (cb < 4 ? cb + (SHARED ? 0u : 4u) : 0x0Cu);
         sel[k] = sa | 0x0C00u | (sb << 16) | 0x0C000000u;
-        Hk[k] = pk2(left(ra), left(rb));
+        Hk[k] = FR ? pk2(fr(left(ra), ra, -1), fr(left(rb), rb, -1)) : pk2(left(ra), left(rb));
         Ek[k] = GOTOH ? (TYPE == NV_LOCAL ? BB : NEG) : 0u;
         msk[k] = ((uint32_t)ra == last_a ? 0x0000FFFFu : 0u) | ((uint32_t)rb == last_b ? 0xFFFF0000u : 0u);
         has_last |= msk[k] != 0u;
@@ -143,13 +154,21 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     uint32_t best = TYPE == NV_LOCAL ? BB : NEG;   // stored; NEG = no cell seen (BestSink, sink_inl.h:38-40)
     // from the lane above: H(r0-1, c), F(r0-1, c), H(r0-1, c-1); rH starts as the
     // left boundary H(r0-1, -1), lane 1's diagonal at column 0 (nvbio.hpp)
-    uint32_t rH = lg == 0 ? BB : pk2(left(ra0 - 1), left(rb0 - 1));
+    uint32_t rH = lg == 0 ? BB
+                : FR ? pk2(fr(left(ra0 - 1), ra0 - 1, -1), fr(left(rb0 - 1), rb0 - 1, -1))
+                     : pk2(left(ra0 - 1), left(rb0 - 1));
+    const uint32_t MISF = (uint32_t)(A.mismatch + g - A.go) * 0x10001u, DL = (uint32_t)dl * 0x10001u;
     uint32_t rF = NEG, pH = BB;
     for (uint32_t s = 0; s < nsteps; ++s) {
         const int32_t c = (int32_t)s - (int32_t)lg;
         uint32_t Hup, Fup, Hdg;
         if (lg == 0) {
-            if (TYPE == NV_GLOBAL) {
+            if (FR) {   // H of the row above the lane's first (-1; BOT: virtual rows per half), in the frame
+                const int32_t hu = TYPE == NV_GLOBAL ? A.go + A.ge * c : 0;
+                const int32_t hd = TYPE == NV_GLOBAL && c >= 1 ? A.go + A.ge * (c - 1) : 0;
+                Hup = pk2(fr(hu, ra0 - 1, c), fr(hu, rb0 - 1, c));
+                Hdg = pk2(fr(hd, ra0 - 1, c - 1), fr(hd, rb0 - 1, c - 1));
+            } else if (TYPE == NV_GLOBAL) {
                 Hup = pk(GOTOH ? A.go + A.ge * c : A.del * (c + 1));
                 Hdg = pk(GOTOH ? (c >= 1 ? A.go + A.ge * (c - 1) : 0) : A.del * c);
             } else { Hup = BB; Hdg = BB; }
@@ -163,7 +182,14 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
                 const uint32_t v = __builtin_amdgcn_perm(T1, T, sel[k]);
                 const uint32_t tmp = Hdg + v + MIS;
                 uint32_t H;
-                if (GOTOH) {
+                if (FR) {
+                    const uint32_t tmp2 = Hdg + v + MISF;
+                    const uint32_t F = pk_max_u16(Fup, Hup);
+                    const uint32_t E = pk_max_u16(Ek[k], Hk[k]);
+                    H = pk_max3(E, F, tmp2) + DL;
+                    Ek[k] = E;
+                    Fup = F;
+                } else if (GOTOH) {
                     const uint32_t F = pk_max3(Fup - GE, Hup - GO, FLOOR);
                     const uint32_t E = pk_max3(Ek[k] - GE, Hk[k] - GO, FLOOR);
                     H = pk_max3(E, F, tmp);
@@ -183,13 +209,20 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
             }
             if (TYPE == NV_LOCAL) best = lbest;
             if (BOT) {
-                if (lg == G - 1) best = pk_max3(best, Hk[R - 1], best);
+                // FR: the row's columns in one frame, + g*(N-1-c) (c < N here)
+                const uint32_t kof = FR ? (uint32_t)(g * (int32_t)(N - 1 - (uint32_t)c)) * 0x10001u : 0u;
+                if (lg == G - 1) best = pk_max3(best, Hk[R - 1] + kof, best);
             } else if (TYPE != NV_LOCAL && has_last) {
-                uint32_t h = 0;
+                uint32_t h = 0, hm = 0;
 #pragma unroll
-                for (int k = 0; k < R; ++k) h |= Hk[k] & msk[k];
+                for (int k = 0; k < R; ++k) { h |= Hk[k] & msk[k]; hm |= msk[k]; }
                 if (TYPE == NV_SEMI) {   // a half without its last row here, or past its text: +0
-                    if (!SHARED) h &= ((uint32_t)c < Na ? 0x0000FFFFu : 0u) | ((uint32_t)c < Nb ? 0xFFFF0000u : 0u);
+                    if (!SHARED) hm &= ((uint32_t)c < Na ? 0x0000FFFFu : 0u) | ((uint32_t)c < Nb ? 0xFFFF0000u : 0u);
+                    // FR: + g*(N-1-c) per half, masked first so that no add carries across
+                    const uint32_t off = FR ? (((uint32_t)(g * (int32_t)(Na - 1 - (uint32_t)c)) & 0xFFFFu) |
+                                               ((uint32_t)(g * (int32_t)(Nb - 1 - (uint32_t)c)) << 16)) & hm
+                                            : 0u;
+                    h = (h & hm) + off;
                     best = pk_max3(best, h, best);
                 } else if (SHARED) {
                     if ((uint32_t)c == N - 1) best = h;
@@ -211,6 +244,7 @@ __global__ __launch_bounds__(256) void nv16_kernel(Nv16Args A) {
     auto out = [&](bool valid, uint32_t pair, uint32_t M, uint32_t N, uint32_t half, bool writer) {
         if (!valid || !writer) return;
         int32_t v = (int32_t)((best >> (16 * half)) & 0xFFFFu) - B;
+        if (FR) v -= dl + g * (int32_t)(M + N - 2);   // the frame at (M-1, N-1); SEMI keys: + g*(N-1-c)
         if (M == 0) {
             v = TYPE == NV_SEMI ? (N ? 0 : INT32_MIN)
               : TYPE == NV_GLOBAL ? (N ? (GOTOH ? A.go + A.ge * (int32_t)(N - 1) : A.del * (int32_t)N) : INT32_MIN)

@@ -50,6 +50,7 @@ struct WfArgs {
     const uint32_t *perm;      // slot -> pair (pairs sorted by step-axis length, dispatch.hip), or NULL
     uint32_t slot0;            // wavefront16 SEMI TAIL=QUERY/BOTH: first slot of this class launch (n = its end)
     uint32_t tb_q8;            // wavefront16 TB kernels: direction chunks of 8 consecutive pairs interleaved (tb_kernel)
+    uint32_t kf16;             // wavefront16 LOCAL: f16-pattern keys over this many columns (0: 16-bit keys H*256 + col)
     const int32_t *stop;       // SEMI TAIL=TARGET reverse pass (start.hpp): per pair, the forward score; the
                                // last-row maximum is then taken inside the first 8-column strip holding a
                                // value >= it (the reference's early exit), else over the whole row

@@ -74,6 +74,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
+#ifndef GX_PROBE_LOCAL
+#define GX_PROBE_LOCAL 0   // step_local timing probes (bit 0: F, bit 1: E without the extension subtract)
+#endif
 #ifndef GX_WF16_CAPTURE_TREE
 #define GX_WF16_CAPTURE_TREE 0   // GLOBAL kernels: branch-free score / start-cell capture
 #endif
@@ -144,13 +147,20 @@ __device__ __forceinline__ Pk16 pk16_params(const WfArgs &A) {
 // to 512 columns (KM != 0) keep a second key per row for columns 256..511:
 // KM = 1 while lanes straddle column 256 (each lane feeds the key of its own
 // column's half, the other gets a 0 candidate), KM = 2 once every lane is past it.
-template <int R, int KM = 0>
+//
+// KU (A.kf16 launches, dispatch.hip): keys as f16 patterns 0x0400 + H*C + (C-1-c),
+// C = the launch's padded target length, so one v_pk_maximum3 folds two columns'
+// candidates into a row's key: KU = 1 (first step of a pair) updates no key, KU = 2
+// takes max3(key, cand(Hin = the previous column's H, invp), cand(H, invn)) — 3
+// instructions per two cells instead of 4 (10.5 per cell pair instead of 11).
+template <int R, int KM = 0, int KU = 0>
 __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const uint32_t diag_top,
                                            const uint32_t f_top, const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                            uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
                                            uint32_t (&key2)[R], uint32_t &f_out, const uint32_t KK,
                                            const uint32_t OEK, const uint32_t EXT, const uint32_t BB,
-                                           const uint32_t KMUL, const uint32_t bshift) {
+                                           const uint32_t KMUL, const uint32_t bshift, const uint32_t invp = 0,
+                                           const uint32_t invn = 0, uint32_t *FL = nullptr) {
     const bool hi = KM != 0 && c >= 256;
     const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
     const uint32_t col2 = (c >= 256 && c < 512) ? (uint32_t)(511 - c) : 0u;
@@ -165,10 +175,31 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
         const uint32_t tmp = pk_subnb(t1, KK);
         const uint32_t toe = pk_subnb(t1, OEK);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
+#if GX_PROBE_LOCAL == 4   // timing probe only (results invalid): the drift-frame instruction mix
+        if (KU != 0) {
+            f = pk_max_u16(toe, f);
+            Ek[k] = pk_max3(toe, Ek[k], FL[k]);
+            FL[k] = FL[k] + EXT;
+            if (KU == 2)
+                key[k] = pk_max3(key[k], pk_mad_u16(Hin[k] - FL[k], KMUL, invp), pk_mad_u16(H - FL[k], KMUL, invn));
+            diag = Hin[k];
+            Hout[k] = H;
+            continue;
+        }
+#endif
+#if GX_PROBE_LOCAL & 2   // timing probes only (results invalid): no E / F extension subtract
+        Ek[k] = pk_max3(toe, Ek[k], BB);
+#else
         Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), BB);
+#endif
+#if GX_PROBE_LOCAL & 1
+        f = pk_max3(toe, f, BB);
+#else
         f = pk_max3(toe, pk_subnb(f, EXT), BB);
-        if (KM != 2) key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmA, invc));
-        if (KM != 0) key2[k] = pk_max_u16(key2[k], pk_mad_u16(H, kmB, invc2));
+#endif
+        if (KU == 2) key[k] = pk_max3(key[k], pk_mad_u16(Hin[k], KMUL, invp), pk_mad_u16(H, KMUL, invn));
+        if (KU == 0 && KM != 2) key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmA, invc));
+        if (KU == 0 && KM != 0) key2[k] = pk_max_u16(key2[k], pk_mad_u16(H, kmB, invc2));
         diag = Hin[k];
         Hout[k] = H;
     }
@@ -608,6 +639,35 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 sweep(std::integral_constant<int, 0>{}, min(nsteps, 256u));
                 sweep(std::integral_constant<int, 1>{}, min(nsteps, 256u + G));
                 sweep(std::integral_constant<int, 2>{}, nsteps);
+            } else if (A.kf16) {
+                // f16-pattern keys (step_local KU): candidate 0x0400 + H*C + (C-1-c) for the
+                // columns c < C, 0x0400 + H*C elsewhere (H = 0 left of the matrix; right of
+                // the padded target no cell beats the real columns' maximum)
+                const uint32_t C = A.kf16, KMC = A.one * C;
+                const uint32_t bC = (uint32_t)P.base * C;
+                auto inv = [&](int32_t cc) {
+                    const uint32_t term = (cc >= 0 && (uint32_t)cc < C) ? C - 1u - (uint32_t)cc : 0u;
+                    return ((0x0400u + term - bC) & 0xFFFFu) * 0x10001u;
+                };
+                uint32_t FL[R];   // GX_PROBE_LOCAL 4 only
+#pragma unroll
+                for (int k = 0; k < R; ++k) { key[k] = 0x04000400u; FL[k] = BB; }
+                for (; s < nsteps; s += 2, c += 2) {
+                    uint2 T = tnext;
+                    tnext = tcol[c + 1 + G];
+                    step_local<R, 0, 1>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, key, f, KK,
+                                        OEK, EXT, BB, KMC, bshift, 0u, 0u, FL);
+                    prevRecvH = recvH;
+                    recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
+                    recvF = (uint32_t)shr_lane((int32_t)f);
+                    T = tnext;
+                    tnext = tcol[c + 2 + G];
+                    step_local<R, 0, 2>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, key, f,
+                                        KK, OEK, EXT, BB, KMC, bshift, inv(c), inv(c + 1), FL);
+                    prevRecvH = recvH;
+                    recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
+                    recvF = (uint32_t)shr_lane((int32_t)f);
+                }
             } else {
                 sweep(std::integral_constant<int, 0>{}, nsteps);
             }
@@ -621,6 +681,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 const uint32_t r = r0 + k;
                 const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
                 uint32_t H = kk >> 8, col = 255u - (kk & 0xFFu);
+                if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c)
+                    const uint32_t C = A.kf16, x = kk - 0x0400u;
+                    H = x / C;
+                    col = C - 1u - (x - H * C);
+                }
                 if constexpr (K2) {   // columns 256..511: later, so they win only when strictly higher
                     const uint32_t k2v = (key2[k] >> (16 * h)) & 0xFFFFu;
                     if ((k2v >> 8) > H) { H = k2v >> 8; col = 511u - (k2v & 0xFFu); }
