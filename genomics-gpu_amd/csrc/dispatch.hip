@@ -319,12 +319,19 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 pl.packed16 = packed16_ok(p, wf_algo, s.max_q, s.max_t, &pl.vmin,
                                           (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8);
             pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
-            // LOCAL score kernels: keys 0x0400 + H*C + (C-1-c) with C = the padded target
-            // length fit the f16 window when (Hmax + 1) * C <= 0x7800 (step_local KU);
-            // GASALX_KF16=0 keeps the 16-bit keys (A/B runs)
+            // LOCAL score kernels in the e-drift frame (wavefront16.hpp step_local_dr): keys
+            // 0x0400 + H*C + (C-1-c) with C = the padded target length need (Hmax + 1) * C
+            // <= 0x7800; values B + H + e(r + c) over the shape's span stay in the window and
+            // the top lane's first diagonal B - 2e above 0x0400.  GASALX_KF16=0 keeps the
+            // round-2 kernel (A/B runs)
             if (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && env_flag("GASALX_KF16", true)) {
-                const int64_t hmax = (int64_t)std::max(p.match, 0) * std::min(q8, t8);
-                if ((hmax + 1) * (int64_t)y8 <= 0x7800) pl.kf16 = y8;
+                const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
+                const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
+                const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
+                const int64_t span = (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8;
+                if ((hmax + 1) * (int64_t)y8 <= 0x7800 && base + hmax + e * span + a + k + 64 <= 0x7BFF &&
+                    base - 2 * e >= 0x400)
+                    pl.kf16 = y8;
             }
             pl.semi_tq = pl.semi_tq && pl.packed16;
         }

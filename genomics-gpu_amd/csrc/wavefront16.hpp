@@ -160,7 +160,7 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
                                            uint32_t (&key2)[R], uint32_t &f_out, const uint32_t KK,
                                            const uint32_t OEK, const uint32_t EXT, const uint32_t BB,
                                            const uint32_t KMUL, const uint32_t bshift, const uint32_t invp = 0,
-                                           const uint32_t invn = 0, uint32_t *FL = nullptr) {
+                                           const uint32_t invn = 0) {
     const bool hi = KM != 0 && c >= 256;
     const uint32_t col = (c >= 0 && c < 256) ? (uint32_t)(255 - c) : 0u;
     const uint32_t col2 = (c >= 256 && c < 512) ? (uint32_t)(511 - c) : 0u;
@@ -175,18 +175,6 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
         const uint32_t tmp = pk_subnb(t1, KK);
         const uint32_t toe = pk_subnb(t1, OEK);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
-#if GX_PROBE_LOCAL == 4   // timing probe only (results invalid): the drift-frame instruction mix
-        if (KU != 0) {
-            f = pk_max_u16(toe, f);
-            Ek[k] = pk_max3(toe, Ek[k], FL[k]);
-            FL[k] = FL[k] + EXT;
-            if (KU == 2)
-                key[k] = pk_max3(key[k], pk_mad_u16(Hin[k] - FL[k], KMUL, invp), pk_mad_u16(H - FL[k], KMUL, invn));
-            diag = Hin[k];
-            Hout[k] = H;
-            continue;
-        }
-#endif
 #if GX_PROBE_LOCAL & 2   // timing probes only (results invalid): no E / F extension subtract
         Ek[k] = pk_max3(toe, Ek[k], BB);
 #else
@@ -200,6 +188,47 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
         if (KU == 2) key[k] = pk_max3(key[k], pk_mad_u16(Hin[k], KMUL, invp), pk_mad_u16(H, KMUL, invn));
         if (KU == 0 && KM != 2) key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmA, invc));
         if (KU == 0 && KM != 0) key2[k] = pk_max_u16(key2[k], pk_mad_u16(H, kmB, invc2));
+        diag = Hin[k];
+        Hout[k] = H;
+    }
+    f_out = f;
+}
+
+// ---------------------------------------------------------------------------
+// LOCAL step in the e-drift frame (A.kf16 launches): cell (r, c) stores value + B +
+// e(r+c), so neither E nor F pays its extension subtract (each one measured at ~9 %
+// of the kernel, profiles/r03_local_drift_ab.md).  The floor at 0 moves with the
+// frame: FL[k] = B + e(r + c + 1), E's floor for the next column, one add per cell
+// off the dependency chains; F is left unfloored (E >= 0 already floors H, and H =
+// max(tmp, E, F) is the same for every F <= 0).  tmp = diag + v - (K - 2e), toe =
+// diag + v - (K - 2e + o).  Keys: the f16 patterns of step_local KU, from H^ less
+// FL - 2e (borrow-free 32-bit subtracts: Hin = H^(r, c) >= FL - 2e, H >= FL - e),
+// two columns per v_pk_maximum3 (KEYS: the second step of a pair).
+// ---------------------------------------------------------------------------
+template <int R, bool KEYS>
+__device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
+                                              const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
+                                              uint32_t (&Ek)[R], uint32_t (&key)[R], uint32_t (&FL)[R],
+                                              uint32_t &f_out, const uint32_t KX, const uint32_t OEX,
+                                              const uint32_t EXT, const uint32_t KMUL, const uint32_t invp,
+                                              const uint32_t invn, const uint32_t EXT2) {
+    uint32_t diag = diag_top, f = f_top;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KX);
+        const uint32_t toe = pk_subnb(t1, OEX);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        Ek[k] = pk_max3(toe, Ek[k], FL[k]);
+        if (KEYS) {
+            // 32-bit subtracts, borrow-free: Hin >= FL - 2e and H >= FL - e
+            const uint32_t g2 = pk_subnb(FL[k], EXT2);
+            const uint32_t d1 = pk_subnb(Hin[k], g2), d2 = pk_subnb(H, g2);
+            key[k] = pk_max3(key[k], pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn));
+        }
+        FL[k] = pk_addnc(FL[k], EXT);
+        f = pk_max_u16(toe, f);
         diag = Hin[k];
         Hout[k] = H;
     }
@@ -640,33 +669,56 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 sweep(std::integral_constant<int, 1>{}, min(nsteps, 256u + G));
                 sweep(std::integral_constant<int, 2>{}, nsteps);
             } else if (A.kf16) {
-                // f16-pattern keys (step_local KU): candidate 0x0400 + H*C + (C-1-c) for the
-                // columns c < C, 0x0400 + H*C elsewhere (H = 0 left of the matrix; right of
-                // the padded target no cell beats the real columns' maximum)
+                // the e-drift frame (step_local_dr); f16-pattern keys 0x0400 + H*C + (C-1-c)
+                // for the columns c < C, 0x0400 + H*C elsewhere (H = 0 left of the matrix;
+                // right of the padded target no cell beats the real columns' maximum).
+                // Lane lg starts at column c0 = -lg with "0 in the frame" everywhere, which
+                // the garbage columns keep exactly (score 0, E at its floor), so they reach
+                // column -1 as the left boundary H = E = 0.  Top lane: diag H(-1, c-1) = 0,
+                // F(0, c) <= 0 (BB).
                 const uint32_t C = A.kf16, KMC = A.one * C;
-                const uint32_t bC = (uint32_t)P.base * C;
-                auto inv = [&](int32_t cc) {
+                const int32_t ge = A.e, pbv = P.base;
+                const uint32_t EXT2 = pk_bcast(2 * ge);
+                const uint32_t KXD = (uint32_t)((P.k - 2 * ge) * 0x10001),
+                               OEXD = (uint32_t)((P.k - 2 * ge + A.o) * 0x10001);
+                auto inv = [&](int32_t cc, uint32_t add) {
                     const uint32_t term = (cc >= 0 && (uint32_t)cc < C) ? C - 1u - (uint32_t)cc : 0u;
-                    return ((0x0400u + term - bC) & 0xFFFFu) * 0x10001u;
+                    return ((0x0400u + term + add * C) & 0xFFFFu) * 0x10001u;
                 };
-                uint32_t FL[R];   // GX_PROBE_LOCAL 4 only
+                // Each lane keeps the frame shifted by its own constant, e(k + s) instead of
+                // e(r + c) (r = lg*R + k, c = s - lg): every floor FL[k] = B + e(k + s + 1) is
+                // then the same in all lanes (scalar registers, s_add per step) and the
+                // values a lane receives from the lane above drop by e(R - 1).
+                uint32_t FL[R];
 #pragma unroll
-                for (int k = 0; k < R; ++k) { key[k] = 0x04000400u; FL[k] = BB; }
+                for (int k = 0; k < R; ++k) {
+                    key[k] = 0x04000400u;
+                    HA[k] = (uint32_t)(pbv + ge * (k - 1)) * 0x10001u;   // H^(r, c0 - 1) = 0
+                    Ek[k] = (uint32_t)(pbv + ge * k) * 0x10001u;         // E^(r, c0) = its floor
+                    FL[k] = (uint32_t)(pbv + ge * (k + 1)) * 0x10001u;   // floor of E(r, c0 + 1)
+                }
+                const uint32_t ADJ = pk_bcast(ge * (R - 1));
+                // the diagonals of the first two steps, which no upper-lane step hands over
+                // (lane 1's upper lane has no garbage column -1): H = 0 at k = -1, s - 1
+                prevRecvH = (uint32_t)(pbv - 2 * ge) * 0x10001u;
+                recvH = (uint32_t)(pbv - ge) * 0x10001u;
                 for (; s < nsteps; s += 2, c += 2) {
                     uint2 T = tnext;
                     tnext = tcol[c + 1 + G];
-                    step_local<R, 0, 1>(T, c, top ? BB : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, key, f, KK,
-                                        OEK, EXT, BB, KMC, bshift, 0u, 0u, FL);
+                    const uint32_t dt0 = (uint32_t)(pbv + ge * (c - 2)) * 0x10001u;   // lane 0: H^(-1, c - 1)
+                    step_local_dr<R, false>(T, top ? dt0 : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, FL, f,
+                                            KXD, OEXD, EXT, KMC, 0u, 0u, EXT2);
                     prevRecvH = recvH;
-                    recvH = (uint32_t)shr_lane((int32_t)HB[R - 1]);
-                    recvF = (uint32_t)shr_lane((int32_t)f);
+                    recvH = pk_subnb((uint32_t)shr_lane((int32_t)HB[R - 1]), ADJ);
+                    recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
                     T = tnext;
                     tnext = tcol[c + 2 + G];
-                    step_local<R, 0, 2>(T, c + 1, top ? BB : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, key, f,
-                                        KK, OEK, EXT, BB, KMC, bshift, inv(c), inv(c + 1), FL);
+                    const uint32_t dt1 = (uint32_t)(pbv + ge * (c - 1)) * 0x10001u;
+                    step_local_dr<R, true>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
+                                           KXD, OEXD, EXT, KMC, inv(c, 0), inv(c + 1, (uint32_t)(-ge)), EXT2);
                     prevRecvH = recvH;
-                    recvH = (uint32_t)shr_lane((int32_t)HA[R - 1]);
-                    recvF = (uint32_t)shr_lane((int32_t)f);
+                    recvH = pk_subnb((uint32_t)shr_lane((int32_t)HA[R - 1]), ADJ);
+                    recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
                 }
             } else {
                 sweep(std::integral_constant<int, 0>{}, nsteps);
