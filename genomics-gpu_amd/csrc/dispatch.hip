@@ -329,9 +329,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
                 const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
                 const int64_t span = (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8;
-                if ((hmax + 1) * (int64_t)y8 <= 0x7800 && base + hmax + e * span + a + k + 64 <= 0x7BFF &&
-                    base - 2 * e >= 0x400)
-                    pl.kf16 = y8;
+                const bool frame = base + hmax + e * span + a + k + 64 <= 0x7BFF && base - 2 * e >= 0x400;
+                if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) pl.kf16 = y8;
             }
             pl.semi_tq = pl.semi_tq && pl.packed16;
         }

@@ -47,6 +47,9 @@ __device__ __forceinline__ float shr_lane_f(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
 }
 __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
+#ifndef GX_HMM_PKFMA
+#define GX_HMM_PKFMA 0   // 1: the I and MM FMAs of a cell as one v_pk_fma_f32 (A/B: 4,574 vs 5,242 GCUPS, r03_pairhmm_ab.md)
+#endif
 #ifndef GX_HMM_WAVES
 #define GX_HMM_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
@@ -93,8 +96,13 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
     // (0, 0, D0) down at every column.
     const int32_t r0 = (int32_t)(lg * RR) - (int32_t)(G * RR) + (int32_t)R;
     uint32_t rb[RR];
-    float qm1[RR], qm3[RR], de[RR], xi[RR], al[RR], dk[RR];
+    float qm1[RR], qm3[RR], xi[RR], dk[RR];
     float Mk[RR], Dk[RR], MM[RR];
+    // GX_HMM_PKFMA: (delta, alpha) of a row side by side, so the cell's two FMAs on MU
+    // (I = MU*delta + I*0.1, MM = alpha*MU + 0.9*(I + D)) issue as one v_pk_fma_f32,
+    // each element rounded as the scalar FMA (exact)
+    typedef float hmf2 __attribute__((ext_vector_type(2)));
+    hmf2 deal[RR];
     const float D0 = valid && H ? __fdiv_rn(c0, (float)H) : 0.f;      // constant[0]/(float)H
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
@@ -116,9 +124,8 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
         other |= in && !acgt(rb[k]);
         qm1[k] = in ? __fsub_rn(1.0f, q) : 0.f;     // Qm_1 = constant[1] - Qm
         qm3[k] = in ? __fdiv_rn(q, 3.0f) : 0.f;     // fdividef(Qm, 3) (<= 2 ulp in the reference)
-        de[k] = d;
+        deal[k] = hmf2{d, a};
         xi[k] = x;
-        al[k] = a;
         dk[k] = in ? c01 : 1.0f;
         Mk[k] = 0.f;
         Dk[k] = in ? 0.f : D0;
@@ -187,9 +194,16 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
                 const float IIMI = __fmul_rn(IU, k == 0 ? c01_0 : c01);
                 const float MIIDD = __fmul_rn(c09, MID);
                 const float Mn = __fmul_rn(aa[k], MM[k]);
-                const float In = __fmaf_rn(MU, de[k], IIMI);
+#if GX_HMM_PKFMA
+                const hmf2 im = __builtin_elementwise_fma(hmf2{MU, MU}, deal[k], hmf2{IIMI, MIIDD});
+                const float In = im.x;
                 const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
-                MM[k] = __fmaf_rn(al[k], MU, MIIDD);
+                MM[k] = im.y;
+#else
+                const float In = __fmaf_rn(MU, deal[k].x, IIMI);
+                const float Dn = __fmaf_rn(Dk[k], dk[k], DDM);
+                MM[k] = __fmaf_rn(deal[k].y, MU, MIIDD);
+#endif
                 Mk[k] = Mn; Dk[k] = Dn;
                 MU = Mn; IU = In; DU = Dn;
             }
