@@ -455,7 +455,7 @@ def end_to_end(eng, kind, data, params, cells, reps=5, seed_score=None):
         return res
     if kind != 5 and params.start_pos == G.WITH_TB:
         host = G.PinnedHost(data.q_bytes)
-        dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, cigar_out=host.array))
+        dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, seed_scores=seeds, cigar_out=host.array))
         host.close()
         res["pinned_cigar"] = {"value": round(cells / dtp / 1e9, 2), "ms_per_batch": round(dtp * 1e3, 3)}
     if True:
@@ -466,7 +466,8 @@ def end_to_end(eng, kind, data, params, cells, reps=5, seed_score=None):
         ht.array[:] = data.t_data
         pb = dataclasses.replace(data, q_data=hq.array, t_data=ht.array)
         hc = G.PinnedHost(data.q_bytes) if params.start_pos == G.WITH_TB else None
-        dtp, _ = timed(lambda: eng.align_host(pb, params, fields=fields, cigar_out=hc.array if hc else None))
+        dtp, _ = timed(lambda: eng.align_host(pb, params, fields=fields, seed_scores=seeds,
+                                              cigar_out=hc.array if hc else None))
         res["pinned_io"] = {"value": round(cells / dtp / 1e9, 2), "ms_per_batch": round(dtp * 1e3, 3),
                             "pinned": "q/t sequence bytes" + (" + CIGAR buffer" if hc else "")}
         for h in (hq, ht, hc):
