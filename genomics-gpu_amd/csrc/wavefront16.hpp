@@ -1024,12 +1024,16 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     if (tail_t && valid[h] && cc == (int32_t)yl[h] - 1) {       // semiglobal :160-178
+                        // columns compared in one frame: cell (yl - 1, col) + e*(G*R - col), the
+                        // old-frame pattern + e*(yl + G*R) (thrp too); positive.  The offset is
+                        // formed here, from an opaque base: R hoisted per-column constants spill
+                        uint32_t fo = (uint32_t)ge * ((uint32_t)(G * R) - r0);
+                        asm volatile("" : "+v"(fo));
 #pragma unroll
                         for (int k = 0; k < R; ++k) {
                             const uint32_t col = r0 + k;
-                            // columns compared in one frame: cell (yl - 1, col) + e*(G*R - col),
-                            // the old-frame pattern + e*(yl + G*R) (thrp too); positive
-                            const uint32_t v = ((Hout[k] >> (16 * h)) & 0xFFFFu) + (uint32_t)ge * ((uint32_t)(G * R) - col);
+                            const uint32_t v = ((Hout[k] >> (16 * h)) & 0xFFFFu) + fo;
+                            fo -= (uint32_t)ge;
                             const uint32_t cand =
                                 col >= xl[h] ? 0u
                                 : (int32_t)v >= thrp[h]
