@@ -74,6 +74,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
+#ifndef GX_SEMI_CHAIN2
+#define GX_SEMI_CHAIN2 0   // step_semi A/B (see there)
+#endif
 #ifndef GX_PROBE_LOCAL
 #define GX_PROBE_LOCAL 0   // step_local timing probes (bit 0: F, bit 1: E without the extension subtract)
 #endif
@@ -390,6 +393,24 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
                                           const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                           uint32_t (&Fk)[R], const uint32_t GO, const uint32_t *pv = nullptr) {
     uint32_t diag = diag_top, h = hl, e = el;
+#if GX_SEMI_CHAIN2
+    // timing A/B: E(r,c) = max(h, e) taken inside the next max3 as a fourth operand, so
+    // the dependency chain per register is sub + max3 instead of max + max3 + sub
+    // (one more instruction per two cells: max(tmp, F) off the chain)
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        if (PV > 0 && k >= R - PV) v = pk_addnc(v, pv[k - (R - PV)]);
+        const uint32_t tmp = pk_addnc(diag, v);
+        Fk[k] = pk_max_u16(Hin[k], Fk[k]);
+        const uint32_t a = pk_max_u16(tmp, Fk[k]);
+        const uint32_t en = pk_max_u16(h, e);                        // E(r,c), off the chain
+        h = pk_subnb(pk_max3(a, h, e), GO);                          // max3(tmp, F, max(h, e)) - o
+        e = en;
+        diag = Hin[k];
+        Hout[k] = h;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
@@ -401,6 +422,7 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
         diag = Hin[k];
         Hout[k] = h;
     }
+#endif
     hl = h;
     el = e;
 }
