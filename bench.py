@@ -696,11 +696,12 @@ def main():
             sets[k][0].align_device_ptrs(params, set_ptrs[k], batch.q_bytes, batch.t_bytes, n, rl, hl,
                                          sets[k][1].cuda_stream)
 
-        def results():
-            r = {f: d[names[f]][:n].cpu().numpy() for f in fields}
+        def results(k=0):
+            dk = d if k == 0 else extra_bufs[k - 1]
+            r = {f: dk[names[f]][:n].cpu().numpy() for f in fields}
             if tb:
-                r["cigar"] = d["cigar"].cpu().numpy()
-                r["n_ops"] = d["n_cigar_ops"].cpu().numpy().view(np.uint32)
+                r["cigar"] = dk["cigar"].cpu().numpy()
+                r["n_ops"] = dk["n_cigar_ops"].cpu().numpy().view(np.uint32)
             return r
     torch.cuda.synchronize(dev)
     synth_s = time.perf_counter() - t_syn
@@ -790,6 +791,17 @@ def main():
                 gsub["n_ops"] = got["n_ops"][:m]
             mism, extra = compare_align(gsub, ref, fields, batch=sub, cigar=tb)
             ref_scores = ref["score"]
+            # --streams S: the other engines aligned the same inputs; their outputs must equal set 0's
+            if n_sets > 1:
+                other = 0
+                for k in range(1, n_sets):
+                    gk = results(k)
+                    gks = {f: gk[f][:m] for f in fields}
+                    if tb:
+                        gks["cigar"] = gk["cigar"][:sub.q_bytes]
+                        gks["n_ops"] = gk["n_ops"][:m]
+                    other += sum(compare_align(gks, gsub, fields, batch=sub, cigar=tb)[0].values())
+                mism["other_streams_vs_set0"] = other
         oracle_s = time.perf_counter() - t_o
         cells_checked = m * rl * ((data.get("band") or hl) if kind == 6 else hl)
         tot = torch.tensor([m, sum(mism.values())], dtype=torch.int64, device=dev)

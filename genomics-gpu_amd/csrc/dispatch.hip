@@ -45,7 +45,7 @@ void Workspace::release_all() {
     for (hipEvent_t *x : {&fork, &join, &dp_done})
         if (*x) { (void)hipEventDestroy(*x); *x = nullptr; }
     for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
-                      &rev_t, &rev_meta, &sort_meta}) b->release();
+                      &rev_t, &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -96,6 +96,15 @@ static WfFn wf16_pick(int G, int R) {
 
 static WfFn wf16_pick_tb(int G, int R) {   // R % 4 == 0 shapes (wavefront16.hpp store groups)
 #define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<WF16_GLOBAL_TB, g, r>;
+    GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
+    GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
+#undef GX_CASE
+    return nullptr;
+}
+
+template <int ALGO>
+static WfFn wf16_pick_r4(int G, int R) {   // R % 4 == 0 shapes (band recomputation)
+#define GX_CASE(g, r) if (G == g && R == r) return &wf16_kernel<ALGO, g, r>;
     GX_CASE(8, 8) GX_CASE(8, 12) GX_CASE(8, 16) GX_CASE(8, 20)
     GX_CASE(16, 16) GX_CASE(16, 20) GX_CASE(32, 20) GX_CASE(64, 20)
 #undef GX_CASE
@@ -333,13 +342,28 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) pl.kf16 = y8;
             }
             pl.semi_tq = pl.semi_tq && pl.packed16;
+            // GLOBAL + traceback: the score sweep stores band checkpoints, a second pass
+            // recomputes each lane's band window with flags, the walk leaves the band only
+            // through the full-matrix fallback (wavefront16.hpp WF16_GLOBAL_CP / _BAND).
+            // GASALX_TB_BAND=0: the full-matrix flags kernel (A/B); GASALX_TB_BAND_W: the
+            // band's half width w (window of lane lg: columns [max(lg*R - w, 0), + R + 2w))
+            if (pl.packed16 && pl.tb && wf_algo == WF_GLOBAL && pl.R16 % 4 == 0 && env_flag("GASALX_TB_BAND", true)) {
+                const char *bw = std::getenv("GASALX_TB_BAND_W");
+                const int w = bw ? std::max(0, std::atoi(bw)) : 12;
+                pl.tb_band = true;
+                pl.band_w = (uint32_t)w;
+                pl.band_wd = ((uint32_t)(pl.R16 + 2 * w) + 3u) & ~3u;
+            }
         }
         const char *an = wf_algo == WF_LOCAL ? (p.start_pos == 1 ? "local_start" : "local")
                        : wf_algo == WF_GLOBAL ? "global"
                        : pl.semi_tq ? "semi_tq" : (p.start_pos == 1 ? "semi_start" : "semi");
         if (pl.packed16)
-            pl.name = std::string("wavefront16_") + an + (pl.tb ? "_tb" : "") + (pl.key2 ? "_k2" : "") + "_G" + std::to_string(pl.G16) + "R" +
-                      std::to_string(pl.R16);
+            // (_nodrift: a LOCAL score plan outside the e-drift frame's window, the round-2 kernel)
+            pl.name = std::string("wavefront16_") + an + (pl.tb ? (pl.tb_band ? "_tbband" : "_tb") : "") +
+                      (pl.key2 ? "_k2" : "") +
+                      (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && !pl.kf16 ? "_nodrift" : "") + "_G" +
+                      std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
         else
             pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
                       std::to_string(pl.G) + "R" + std::to_string(pl.R);
@@ -403,13 +427,23 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             HIPCHK(ws.aux.reserve((size_t)n * 4));
             P16.tbfix = ws.aux.as<int32_t>();
         }
-        WfFn f16 = wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2);
+        WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
+                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2);
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)pl.lds16_bytes));
         hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
         HIPCHK(hipGetLastError());
+        if (pl.tb_band) {   // the band pass over the blocks the sweep aligned (same grid and slots)
+            WfFn fb = wf16_pick_r4<WF16_GLOBAL_BAND>(pl.G16, pl.R16);
+            if (!fb) { set_error("no packed band instance"); return GASALX_EUNSUPPORTED; }
+            if (pl.lds16_bytes > 64 * 1024)
+                HIPCHK(hipFuncSetAttribute((const void *)fb, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)pl.lds16_bytes));
+            hipLaunchKernelGGL(fb, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
+            HIPCHK(hipGetLastError());
+        }
         // ... and the int32 kernel aligns the pairs of the blocks it declined
         A.skip = ws.misc.as<uint8_t>();
         A.skip_ppb = ppb16;
@@ -814,9 +848,10 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
 
     const uint32_t *slot_of = nullptr;   // pair -> slot when the wavefront launch ran sorted
     uint32_t tb_q8 = 0;                  // the packed TB kernels' interleaved layout
+    WfArgs A;                            // the wavefront launch (kept for the traceback fallback)
+    std::memset(&A, 0, sizeof(A));
+    uint32_t *fb_count = nullptr;        // band traceback: pairs handed to the full-matrix fallback
     if (pl.kind == PLAN_WAVEFRONT) {
-        WfArgs A;
-        std::memset(&A, 0, sizeof(A));
         A.q = qsrc; A.t = tsrc;
         A.qoff = b.q_offsets; A.toff = b.t_offsets; A.qlen = b.q_lens; A.tlen = b.t_lens;
         A.score = out.aln_score;
@@ -850,8 +885,23 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         }
         // unsorted waves hold consecutive pairs: interleave their direction chunks
         // (GASALX_TB_Q8=0: per-pair layout, A/B)
-        A.tb_q8 = (pl.packed16 && pl.tb && !A.perm && env_flag("GASALX_TB_Q8", true)) ? 1u : 0u;
+        A.tb_q8 = (pl.packed16 && pl.tb && !pl.tb_band && !A.perm && env_flag("GASALX_TB_Q8", true)) ? 1u : 0u;
         tb_q8 = A.tb_q8;
+        if (pl.tb_band && runs_tb) {
+            // band recomputation buffers per wave of the packed launch (wavefront16.hpp)
+            const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
+            const uint64_t waves = (uint64_t)grid_for(n, ppb16) * kWavesPerBlock;
+            HIPCHK(ws.band_cp.reserve(waves * 2 * pl.R16 * 64 * 4 + 64));
+            HIPCHK(ws.band_stm.reserve(waves * (pl.band_wd + 1) * 64 * 8 + 64));
+            HIPCHK(ws.band_fl.reserve(waves * 64 * (pl.band_wd / 4) * (pl.R16 / 4) * 16 + 64));
+            HIPCHK(ws.band_fb.reserve((size_t)n * 4 + grid_for(n, ppb16) + 256));
+            A.cp = ws.band_cp.as<uint32_t>();
+            A.stm = ws.band_stm.as<uint2>();
+            A.bflags = ws.band_fl.as<uint4>();
+            A.band_w = pl.band_w;
+            A.band_wd = pl.band_wd;
+            fb_count = ws.band_fb.as<uint32_t>();
+        }
         int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start && dp) {
@@ -1060,8 +1110,45 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.pk_fix = ws.aux.as<int32_t>();
             T.pk_q8 = tb_q8;
         }
+        T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1;
+        T.fb_list = T.fb_count = nullptr;
+        T.list = T.n_dev = nullptr;
+        if (fb_count) {
+            T.band = ws.band_fl.as<uint4>();
+            T.band_w = pl.band_w; T.band_wd = pl.band_wd;
+            T.pk_ppw = 2 * (64 / pl.G16);
+            T.fb_count = fb_count;
+            T.fb_list = fb_count + 64;
+            HIPCHK(hipMemsetAsync(fb_count, 0, 4, st));
+        }
         tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
         HIPCHK(hipGetLastError());
+        if (fb_count) {
+            // pairs whose path left the band: the full-matrix packed traceback kernel over the
+            // list (slots = list positions; per-pair flag layout), its int32 kernel for any block
+            // it declines, and the walk again
+            Plan fp = pl;
+            fp.tb_band = false;
+            WfArgs F = A;
+            // the band walk has written CIGAR prefixes over the query batch when that is the
+            // CIGAR buffer (get_tb.h:94): the DP reads align_device's copy of the codes then
+            if (walk_qseq) F.q = walk_qseq;
+            F.perm = T.fb_list;
+            F.n_dev = fb_count;
+            F.tb_q8 = 0;
+            F.cp = nullptr; F.stm = nullptr; F.bflags = nullptr;
+            int rc = launch_wavefront(ws, fp, p, F, st);
+            if (rc) return rc;
+            TbArgs T2 = T;
+            T2.band = nullptr;
+            T2.list = T.fb_list;
+            T2.n_dev = fb_count;
+            T2.slot_of = nullptr;
+            T2.pk_q8 = 0;
+            T2.fb_list = T2.fb_count = nullptr;
+            tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T2);
+            HIPCHK(hipGetLastError());
+        }
     }
     return GASALX_OK;
 }

@@ -34,6 +34,8 @@ struct Workspace {
     DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
     DevBuf rev_q, rev_t, rev_meta;  // WITH_START: reversed slots, their offsets/lengths, reverse results
     DevBuf sort_meta;               // length sort of the forward pass: perm, inverse, histogram
+    DevBuf band_cp, band_stm, band_fl;   // GLOBAL+TB band recomputation: checkpoints, hand-offs, flags
+    DevBuf band_fb;                 // its fallback: count, then the list of pairs, then the launch's flags
     // traceback batches in chunks (align_device, GASALX_TB_CHUNKS): DPs on the
     // caller's stream, walks on walk_stream; one workspace per further chunk; all
     // created on first use
@@ -64,6 +66,8 @@ struct Plan {
     bool band16 = false;    // banded: two pairs per lane in 16-bit halves (banded16.hpp), int32 fallback
     bool local16 = false;   // LOCAL second best: two pairs per lane in 16-bit halves (local16.hpp), int32 fallback
     bool semi_tq = false;   // SEMI TAIL=QUERY/BOTH: packed class launches (one per padded target length), int32 fallback
+    bool tb_band = false;   // packed GLOBAL+TB by band recomputation (wavefront16.hpp WF16_GLOBAL_CP / _BAND)
+    uint32_t band_w = 0, band_wd = 0;
     std::string name;
 };
 

@@ -584,6 +584,15 @@ struct TbArgs {
     const uint8_t *qseq, *tseq;
     const uint32_t *toff;
     int32_t seq_packed, nval, has_npen, npen;
+    // band recomputation (wavefront16.hpp WF16_GLOBAL_BAND): packed pairs read the flags of
+    // their lane's band window ([wave][64][wd/4][R/4] uint4, two pairs per entry); a path that
+    // leaves the band appends its pair to fb_list and stops (its bytes so far are a prefix of
+    // the CIGAR the full-matrix walk writes later)
+    const uint4 *band;
+    uint32_t band_w, band_wd, pk_ppw;   // pk_ppw: pairs (slots) per wave of the DP launch
+    uint32_t *fb_list, *fb_count;
+    // fallback walk: thread tid walks pair list[tid], tid < *n_dev; its slot in the DP launch is tid
+    const uint32_t *list, *n_dev;
 };
 
 // 8 codes of a sequence cached per thread (the walk moves one position at a time)
@@ -603,8 +612,10 @@ __device__ __forceinline__ uint32_t pick4(const uint4 &c, uint32_t k) {
 }
 
 __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= A.n) return;
+    const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t0 >= A.n || (A.n_dev && t0 >= *A.n_dev)) return;
+    const uint32_t tid = A.list ? A.list[t0] : t0;                          // the pair
+    const uint32_t slot = A.list ? t0 : (A.slot_of ? A.slot_of[tid] : tid);   // its slot in the DP launch
     const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
     const uint32_t q8 = (ql + 7) & ~7u, tstrips = (tl + 7) >> 3;
     const uint32_t *tb = A.tb + (uint64_t)tid * A.tb_pair_words;
@@ -612,7 +623,14 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int i, j, total = 0, curr = 0;
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
     else { i = (int)tl; j = (int)ql; }
-    const bool pk = A.pk_flags && A.pk_flags[(A.slot_of ? A.slot_of[tid] : tid) / A.pk_ppb];
+    const bool pk = A.pk_flags && A.pk_flags[slot / A.pk_ppb];
+    const bool bnd = pk && A.band;
+    // band layout: this pair's half of its lane group's entries in wave slot / pk_ppw
+    const uint2 *bnd2 = bnd ? reinterpret_cast<const uint2 *>(A.band) +
+                                  ((uint64_t)(slot / A.pk_ppw) * 64 + ((slot % A.pk_ppw) >> 1) * A.pk_G) *
+                                      ((A.band_wd / 4) * (A.pk_R / 4)) * 2 + (slot & 1u)
+                            : nullptr;
+    bool out_of_band = false;
     // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
     // pair at 8 * c + (tid & 7)
     const bool il8 = pk && A.pk_q8;
@@ -643,7 +661,29 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                        c7 = (uint32_t)i & 7u;
         uint32_t cell_op = 0;   // past the padded grid: 0
         if (strip < tstrips) {
-            if (pk) {
+            if (bnd) {
+                // band window of the row's lane: columns [L, L + wd), flags of 4 x 4 chunks
+                const uint32_t col = strip * 8 + c7;
+                const uint32_t lane = __umulhi(row, A.pk_rmagic), k = row - lane * A.pk_R;
+                const int32_t L = max((int32_t)(lane * A.pk_R) - (int32_t)A.band_w, 0);
+                const uint32_t t = (uint32_t)((int32_t)col - L);
+                if (t >= A.band_wd) { out_of_band = true; break; }
+                const int64_t key = (((int64_t)lane * (A.band_wd / 4) + (t >> 2)) * (A.pk_R / 4) + (k >> 2)) * 2;
+                if (key != chunk_key) {
+                    const uint2 c2 = bnd2[key];
+                    chunk = make_uint4(c2.x, c2.y, 0u, 0u);
+                    chunk_key = key;
+                }
+                const uint32_t fl = (((k & 2u) ? chunk.y : chunk.x) >> (16 * (k & 1u) + (t & 3u))) & 0xFFFFu;
+                const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
+                const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
+                int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
+                if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
+                const uint32_t u = fix_diag ? 0u : (fl & 1u);
+                fix_diag = false;
+                cell_op = (u ? ((fl & 16u) ? 2u : 3u) : (sc < 0 ? 1u : 0u)) | ((fl & 256u) ? 0u : 4u) |
+                          ((fl & 4096u) ? 0u : 8u);
+            } else if (pk) {
                 // wavefront16.hpp step_global_tb flags -> the reference's nibble
                 // window (column + lane) / 4 holds G*R entries, row lane*R + k at
                 // ((k/4)*G + lane)*4 + k%4 (wavefront16.hpp): 4 rows per 8-byte chunk
@@ -694,6 +734,10 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
         prev = opf;
         i = (opf == 0 || opf == 1 || opf == 2) ? i - 1 : i;
         j = (opf == 0 || opf == 1 || opf == 3) ? j - 1 : j;
+    }
+    if (out_of_band) {   // the full-matrix fallback walks this pair again (dispatch.hip)
+        A.fb_list[atomicAdd(A.fb_count, 1u)] = tid;
+        return;
     }
     put(off++, prev | (uint32_t)(count << 2));
     n_ops++;

@@ -111,6 +111,15 @@ std::vector<uint32_t> rebase(const uint32_t *off, uint32_t s, uint32_t e, uint64
 
 template <class T> T *at(T *p, uint64_t k) { return p ? p + k : nullptr; }
 
+// the calling thread's current device, restored when the guard leaves scope (engine
+// creation and ncclCommInitAll switch devices)
+struct DeviceGuard {
+    int dev = -1;
+    bool had = false;
+    DeviceGuard() { had = hipGetDevice(&dev) == hipSuccess; }
+    ~DeviceGuard() { if (had) (void)hipSetDevice(dev); }
+};
+
 }  // namespace
 
 struct gasalx_multi {
@@ -172,6 +181,7 @@ int gasalx_multi_create(const int *devices, int n_devices, uint32_t flags, gasal
             gx::set_error("gasalx_multi_create: device " + std::to_string(devices[i]) + " of " + std::to_string(count));
             return GASALX_EINVAL;
         }
+    DeviceGuard guard;
     gasalx_multi *m = new (std::nothrow) gasalx_multi();
     if (!m) return GASALX_ENOMEM;
     m->devices.assign(devices, devices + n_devices);
@@ -337,7 +347,18 @@ int gasalx_multi_pairhmm_quals_host(gasalx_multi *m, const gasalx_hmm_qual_batch
     });
 }
 
+// (the calling thread's current device is restored on every exit: a torch caller's
+// current_device must not move to the last entry's device)
+static int multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
+                           void *const *streams);
+
 int gasalx_multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
+                           void *const *streams) {
+    DeviceGuard guard;
+    return multi_allgather(m, send, recv, bytes, streams);
+}
+
+static int multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
                            void *const *streams) {
     if (!m || !send || !recv) { gx::set_error("null argument"); return GASALX_EINVAL; }
     const int nd = (int)m->engines.size();
@@ -351,7 +372,11 @@ int gasalx_multi_allgather(gasalx_multi *m, const void *const *send, void *const
         const Rccl &r = rccl();
         ncclResult_t res = r.group_start();
         for (int i = 0; i < nd && res == ncclSuccess; i++) {
-            if (hipSetDevice(m->devices[i]) != hipSuccess) { gx::set_error("hipSetDevice"); return GASALX_EDEVICE; }
+            if (hipSetDevice(m->devices[i]) != hipSuccess) {
+                (void)r.group_end();   // never leave the thread's RCCL group open
+                gx::set_error("hipSetDevice");
+                return GASALX_EDEVICE;
+            }
             res = r.all_gather(send[i], recv[i], bytes, ncclUint8, m->comms[i], st[i]);
         }
         const ncclResult_t end = r.group_end();

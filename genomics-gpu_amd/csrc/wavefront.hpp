@@ -54,7 +54,15 @@ struct WfArgs {
     const int32_t *stop;       // SEMI TAIL=TARGET reverse pass (start.hpp): per pair, the forward score; the
                                // last-row maximum is then taken inside the first 8-column strip holding a
                                // value >= it (the reference's early exit), else over the whole row
-
+    // GLOBAL + traceback by band recomputation (wavefront16.hpp WF16_GLOBAL_CP / WF16_GLOBAL_BAND):
+    // per wave, the left-edge state of every lane's band window (cp: [wave][64][2R] words) and the
+    // bottom-row hand-off of every lane over the window of the lane below (stm: [wave][wd+1][64]),
+    // then the band's direction flags (bflags: [wave][64 lanes][wd/4 windows][R/4] uint4)
+    uint32_t *cp;
+    uint2 *stm;
+    uint4 *bflags;
+    uint32_t band_w, band_wd;  // lane lg's window: columns [max(lg*R - band_w, 0), + band_wd), band_wd % 4 == 0
+    const uint32_t *n_dev;     // when set: the launch's pair count is *n_dev (<= n; traceback fallback list)
 };
 
 constexpr int kWavesPerBlock = 4;
@@ -348,7 +356,8 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * P;
     const uint32_t idx = pair0 + slot;   // slot; the pair is perm[slot] when sorted
     // pairs the packed kernel already aligned are skipped (dispatch.hip); its flags are per block of slots
-    const bool valid = idx < A.n && !(A.skip && A.skip[idx / A.skip_ppb]);
+    const uint32_t nn = A.n_dev ? min(*A.n_dev, A.n) : A.n;   // (traceback fallback: a device-side count)
+    const bool valid = idx < nn && !(A.skip && A.skip[idx / A.skip_ppb]);
     const uint32_t pair = (valid && A.perm) ? A.perm[idx] : idx;
     if (A.skip && !__syncthreads_or(valid)) return;      // block-uniform early exit
 

@@ -248,7 +248,9 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
 // KX = K - 2e >= 0 (K = max(2*ceil(max(b, npen)/2), 2e)); toe = diag + v - (KX +
 // OE - e).  7 instructions per two cells (8 with the round-2 drift K/2, which
 // left an extension add).  32-bit adds/subtracts of per-half constants, exact.
-template <int R>
+// SYNC: row by row (an empty asm ties each row's E and F): the band kernels' sweeps, whose
+// consecutive steps are independent of each other, were otherwise scheduled into spills
+template <int R, bool SYNC = false>
 __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                             const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                             uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t KX,
@@ -265,6 +267,7 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
         f = pk_max3(toe, f, NN);
         diag = Hin[k];
         Hout[k] = H;
+        if (SYNC) asm volatile("" : "+v"(Ek[k]), "+v"(f));
     }
     f_out = f;
 }
@@ -299,7 +302,7 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
     return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA);
 }
 
-template <int R>
+template <int R, bool SYNC = false>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                                uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&dw)[R],
@@ -329,6 +332,9 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
 #if GX_WF16_TB_ROWSYNC
         asm volatile("" : "+v"(f), "+v"(tx), "+v"(ty));   // schedule row by row (tuning variant)
 #endif
+        // SYNC: each row's flags before the next row (the band pass deferred them all to the
+        // window's store otherwise: 345 spilled VGPRs; 120 VGPRs with it)
+        if (SYNC) asm volatile("" : "+v"(dw[k]), "+v"(f));
     }
     f_out = f;
 }
@@ -478,6 +484,18 @@ constexpr int WF16_GLOBAL_TB = 3;     // GLOBAL with traceback words (wavefront1
 constexpr int WF16_LOCAL_TB = 4;      // LOCAL with traceback words (wavefront16 only)
 constexpr int WF16_LOCAL_K2 = 5;      // LOCAL, padded targets of 257..512 columns (two keys per row)
 constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last padded column's rows (Q11)
+// GLOBAL + traceback by band recomputation (dispatch.hip, plan tb_band):
+//  * WF16_GLOBAL_CP: the score-only GLOBAL sweep (step_global, no flags) that also stores, for
+//    every lane lg, its R rows' (H, E) at the column left of its band window [L, L + wd), L =
+//    max(lg*R - w, 0), and its bottom row's hand-off (H, F) over the window of the lane below;
+//  * WF16_GLOBAL_BAND: every lane recomputes its R x wd window from those values alone, with
+//    the direction flags of step_global_tb (identical inputs, identical flags), one 4-column
+//    window of flags at a time into bflags.  tb_kernel walks the band and hands the pairs whose
+//    path leaves it to a WF16_GLOBAL_TB launch over the full matrix (dispatch.hip).
+// Per cell pair the sweep issues 7 instructions instead of step_global_tb's 15; the band is
+// R x wd of every lane's G*R x (ypad) cells (config 3, w = 12: 44 of 304 columns).
+constexpr int WF16_GLOBAL_CP = 7;
+constexpr int WF16_GLOBAL_BAND = 8;
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -485,33 +503,49 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 #define GX_WF16_TQ_BIG_WAVES 3   // R > 20 (A/B knob): 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
 #endif
 
+#ifndef GX_WF16_CP_WAVES
+#define GX_WF16_CP_WAVES 3    // GLOBAL score sweep with band checkpoints
+#endif
+#ifndef GX_WF16_BAND_WAVES
+#define GX_WF16_BAND_WAVES 4  // band recomputation with flags (122 VGPRs)
+#endif
+
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                    : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
                                    : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES
                                    : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? GX_WF16_TQ_BIG_WAVES : GX_WF16_TQ_WAVES)
+                                   : ALGO_ == WF16_GLOBAL_CP ? GX_WF16_CP_WAVES
+                                   : ALGO_ == WF16_GLOBAL_BAND ? GX_WF16_BAND_WAVES
                                    : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
+    constexpr bool GCP = ALGO_ == WF16_GLOBAL_CP;
+    constexpr bool GBD = ALGO_ == WF16_GLOBAL_BAND;
+    constexpr bool GT = GTB || GCP || GBD;   // the traceback kernels' declines and start-cell capture
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
     // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
-    constexpr int ALGO = GTB ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : TQ ? WF_SEMI : ALGO_;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : TQ ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1), slot = lane / G;
-    const uint32_t pair0 = (TQ ? A.slot0 : 0u) + (blockIdx.x * kWavesPerBlock + wave) * (2 * S);
+    // a launch over a device-side count (the traceback fallback list): whole blocks past it leave
+    const uint32_t nn = A.n_dev ? min(*A.n_dev, A.n) : A.n;
+    if (A.n_dev && blockIdx.x * (uint32_t)(kWavesPerBlock * 2 * S) >= nn) return;
+    const uint32_t wv = blockIdx.x * kWavesPerBlock + wave;   // wave index of the launch
+    const uint32_t pair0 = (TQ ? A.slot0 : 0u) + wv * (2 * S);
     uint32_t pr[2], xl[2], yl[2], xo[2], yo[2], xpad[2], ypad[2];
     bool valid[2];
     const uint8_t *X = TR ? A.t : A.q, *Y = TR ? A.q : A.t;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const uint32_t idx = pair0 + 2 * slot + h;   // slot; the pair is perm[slot] when sorted
-        valid[h] = idx < A.n;
+        valid[h] = idx < nn;
         pr[h] = (valid[h] && A.perm) ? A.perm[idx] : idx;
         const uint32_t ql = valid[h] ? A.qlen[pr[h]] : 0, tl = valid[h] ? A.tlen[pr[h]] : 0;
         const uint32_t qo = valid[h] ? A.qoff[pr[h]] : 0, to = valid[h] ? A.toff[pr[h]] : 0;
@@ -546,7 +580,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
-            const uint32_t ylen = GTB ? __shfl(yl[h], ps * G) : 0u;
+            const uint32_t ylen = GT ? __shfl(yl[h], ps * G) : 0u;
             uint32_t v = 0;
             const bool in = (int32_t)y0 >= 0 && y0 < yp;
             if (in) v = load4_codes(Y, yof, y0 >> 2, A.packed);
@@ -556,8 +590,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 other |= l == 5;
                 // traceback reads the first pad query row, scored here as -K: exact for
                 // pad x base columns, not for pad x real-N columns (N == N is a match)
-                if (GTB && !A.has_npen) other |= l == 4 && y0 + j < ylen;
-                if (GTB) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
+                if (GT && !A.has_npen) other |= l == 4 && y0 + j < ylen;
+                if (GT) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
                 tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
             }
         }
@@ -583,7 +617,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T
                     xs[k] = (xs[k] & ~(0xFFu << (16 * h))) | ((l + 4 * h) << (16 * h));
-                } else if (ALGO == WF_LOCAL || GTB || TQ) {
+                } else if (ALGO == WF_LOCAL || GT || TQ) {
                     other |= l != 4;                 // pads must be N (LOCAL: scored -K here, dominated;
                 }                                    // TQ: scored by the N rule through pv)
             }
@@ -612,7 +646,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (valid[h]) A.handled[pair0 + 2 * slot + h] = fast ? 1 : 0;
-    } else if (threadIdx.x == 0) {
+    } else if (threadIdx.x == 0 && !GBD) {               // (the band pass repeats its sweep's verdict)
         A.handled[blockIdx.x] = fast ? 1 : 0;
     }
     if (!fast) return;                                   // the int32 kernel takes this block
@@ -625,6 +659,69 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     const uint32_t NN = (uint32_t)P.neg * 0x10001u;
     const bool top = lg == 0;
     int32_t c = -(int32_t)lg;                            // step-axis position of this lane
+
+    if constexpr (GBD) {
+        // Band recomputation (WF16_GLOBAL_BAND): lane lg's rows r0..r0+R-1 over the columns
+        // [L, L + wd), L = max(r0 - w, 0), from the state WF16_GLOBAL_CP stored (same frame,
+        // same tables, so step_global_tb sees the inputs the full traceback sweep would).
+        // Entering column L: H(r, L - 1) and E(r, L) of the lane's rows (the left boundary of
+        // global.h:57-60 when L = 0); per column c: the upper lane's H(r0 - 1, c - 1) and
+        // F(r0, c) (stream entries c - L and c - L + 1), or the top boundary for lane 0.
+        static_assert(R % 4 == 0, "band windows store flags in groups of 4 rows");
+        const int32_t pb = P.base, go = A.o, ge = A.e, D = P.drift;
+        const uint32_t KX = pk_bcast(P.k - 2 * D), OEX = pk_bcast(P.k - 2 * D + A.o + A.e - D);
+        const uint32_t WD = A.band_wd;
+        const int32_t L = max((int32_t)r0 - (int32_t)A.band_w, 0);
+        // (element by element: a whole-array copy here became one <R x i32> value, a register
+        // tuple the allocator could only place by spilling ~350 VGPRs)
+        uint32_t HA[R], HB[R], Ek[R], dw[R];
+        const uint32_t *cpw = A.cp + ((size_t)wv * 64 + lane) * (2 * R);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const int32_t r = (int32_t)r0 + k;
+            // H(r, -1) (Q2) at anti-diagonal r - 1, E(r, 0) = -inf; else the sweep's checkpoint
+            HA[k] = L == 0 ? (uint32_t)(pb + D * (r - 1) - (r <= 0 ? 0 : go + ge * r)) * 0x10001u : cpw[k];
+            Ek[k] = L == 0 ? NN : cpw[R + k];
+            HB[k] = HA[k];
+            dw[k] = 0;
+        }
+        // the upper lane's stream, two entries ahead (lane 0 reads a neighbour's and ignores it)
+        const uint2 *sp = A.stm + (size_t)wv * (WD + 1) * 64 + (lane ? lane - 1 : 0);
+        uint2 e0 = sp[0], e1 = sp[64], e2 = sp[128];
+        // a window from column 0 starts at the left boundary: H(r0 - 1, -1) (Q2; lane 0 of the
+        // sweep never runs column -1, so lane 1's entry 0 is not stored)
+        if (L == 0) e0.x = (uint32_t)(pb + D * ((int32_t)r0 - 2) - (r0 <= 1 ? 0 : go + ge * ((int32_t)r0 - 1))) * 0x10001u;
+        uint4 *bf = A.bflags + ((size_t)wv * 64 + lane) * (WD / 4) * (R / 4);
+        const bool any = valid[0] || valid[1];
+        c = L;
+        uint32_t fdummy = NN;
+        auto bstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R], const uint32_t t) {
+            const uint2 T = tcol[c + G];
+            // H(-1, c - 1) at anti-diagonal c - 2 (the GLOBAL branch's dtop)
+            const uint32_t dtop = (uint32_t)(pb + D * (c - 2) - (c <= 0 ? 0 : go + ge * c)) * 0x10001u;
+            step_global_tb<R, true>(T, top ? dtop : e0.x, top ? NN : e1.y, xs, Hin, Hout, Ek, dw, fdummy, KX, OEX, NN, j);
+            e0 = e1;
+            e1 = e2;
+            e2 = sp[(size_t)min(t + 3, WD) * 64];
+            ++c;
+        };
+        for (uint32_t t = 0; t < WD; t += 4) {
+            bstep(0, HA, HB, t);
+            bstep(1, HB, HA, t + 1);
+            bstep(2, HA, HB, t + 2);
+            bstep(3, HB, HA, t + 3);
+            if (any) {
+                uint4 *dst = bf + (t / 4) * (R / 4);
+#pragma unroll
+                for (int k = 0; k < R; k += 4)
+                    dst[k / 4] = make_uint4(__builtin_amdgcn_perm(dw[k + 1], dw[k], 0x05040100u),
+                                            __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x05040100u),
+                                            __builtin_amdgcn_perm(dw[k + 1], dw[k], 0x07060302u),
+                                            __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x07060302u));
+            }
+        }
+        return;
+    }
 
     if (ALGO == WF_LOCAL) {
         const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
@@ -814,10 +911,20 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             // traceback starts at (row ql, column tl); when both are pad
             // positions this kernel scores that cell -K instead of N==N, and records
             // its H so tb_kernel can redo the cell's low two bits
-            fixable[h] = GTB && valid[h] && xl[h] < xpad[h] && yl[h] < ypad[h];
+            fixable[h] = GT && valid[h] && xl[h] < xpad[h] && yl[h] < ypad[h];
             kp_lane[h] = xl[h] / R;
             kp[h] = xl[h] - kp_lane[h] * R;
         }
+        // GCP: lane lg's band window starts at column L = max(r0 - w, 0): its rows' H(r, L - 1)
+        // and E(r, L) are stored after the step at column L - 1 (none when L = 0: the left
+        // boundary); the lane below's window starts at Ld = max(r0 + R - w, 0), and this lane's
+        // bottom-row hand-off (H(r0 + R - 1, c), F(r0 + R, c)) is stored for c in [Ld - 1, Ld + wd]
+        const int32_t cs_own = GCP ? max((int32_t)r0 - (int32_t)A.band_w, 0) - 1 : -1;
+        const int32_t cs_dn = GCP ? max((int32_t)(r0 + R) - (int32_t)A.band_w, 0) - 1 : 0;
+        const bool cp_on = GCP && (valid[0] || valid[1]);
+        const bool st_on = cp_on && lg + 1 < G;
+        uint32_t *cpw = GCP ? A.cp + ((size_t)wv * 64 + lane) * (2 * R) : nullptr;   // [wave][lane][2R]
+        uint2 *stw = GCP ? A.stm + (size_t)wv * (A.band_wd + 1) * 64 + lane : nullptr;
         uint2 tnext = tcol[c + G];
         auto half_step = [&](const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
             const uint2 T = tnext;
@@ -839,7 +946,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     step_global_tb<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, dw, f, KX,
                                       OEX, NN, j);
                 else
-                    step_global<R>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KX, OEX, NN);
+                    step_global<R, GCP>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KX, OEX, NN);
 #if GX_WF16_CAPTURE_TREE
                 // branch-free capture: every lane picks one register by a select tree
                 // over the bits of its index (score: row xl - 1 at column yl - 1; fix:
@@ -847,7 +954,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // more VGPRs
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const bool late = GTB && cc >= (int32_t)yl[h];
+                    const bool late = GT && cc >= (int32_t)yl[h];
                     const uint32_t idx = late ? kp[h] : kq[h];
                     uint32_t t[R];
 #pragma unroll
@@ -859,7 +966,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                         for (int k = 0; k + bb < R; k += 2 * bb) t[k] = bit ? t[k + bb] : t[k];
                     }
                     capq[h] = cc == (int32_t)yl[h] - 1 ? t[0] : capq[h];
-                    if (GTB) capp[h] = cc == (int32_t)yl[h] ? t[0] : capp[h];
+                    if (GT) capp[h] = cc == (int32_t)yl[h] ? t[0] : capp[h];
                 }
             }
 #else
@@ -880,6 +987,17 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 }
             }
 #endif
+            if constexpr (GCP) {
+                if (cp_on && cc == cs_own) {
+#pragma unroll
+                    for (int k = 0; k < R; k += 2) {
+                        *reinterpret_cast<uint2 *>(cpw + k) = make_uint2(Hout[k], Hout[k + 1]);
+                        *reinterpret_cast<uint2 *>(cpw + R + k) = make_uint2(Ek[k], Ek[k + 1]);
+                    }
+                }
+                const uint32_t t = (uint32_t)(cc - cs_dn);
+                if (st_on && t <= A.band_wd) stw[(size_t)t * 64] = make_uint2(Hout[R - 1], f);
+            }
             prevRecvH = recvH;
             recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
             recvF = (uint32_t)shr_lane((int32_t)f);
@@ -953,6 +1071,16 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
                 half_step(c, 0, HA, HB);
                 half_step(c + 1, 1, HB, HA);
+            }
+            if constexpr (GCP) {
+#if GX_WF16_CAPTURE_TREE
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    fixv[h] = (int32_t)((capp[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
+#endif
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    if (fixable[h] && lg == kp_lane[h]) A.tbfix[pr[h]] = fixv[h];
             }
         }
 #if GX_WF16_CAPTURE_TREE

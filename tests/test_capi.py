@@ -78,7 +78,7 @@ def test_plan_selection_cpu_only():
         "generic_local"
     assert G.describe_plan(G.make_params(algo=G.KSW), 150, 150) == "generic_ksw"
     assert G.describe_plan(G.make_params(algo=G.GLOBAL, start_pos=G.WITH_TB), 300, 300) == \
-        "wavefront16_global_tb_G16R20"
+        "wavefront16_global_tbband_G16R20"
     assert G.describe_plan(G.make_params(algo=G.UNKNOWN), 10, 10) == "none"
 
 

@@ -745,6 +745,31 @@ def test_packed_global_traceback(engine, scores, alphabet):
     check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
 
 
+@pytest.mark.parametrize("w", ["0", "3", "12", "40"])
+@pytest.mark.parametrize("n,lens", [(700, (20, 310, 20, 310)), (5000, (100, 300, 60, 320)), (333, (1, 40, 1, 40))])
+def test_global_traceback_band_and_fallback(engine, monkeypatch, w, n, lens):
+    # GLOBAL+TB by band recomputation (wavefront16.hpp WF16_GLOBAL_CP / _BAND): paths that leave
+    # a lane's window go to the full-matrix fallback; w = 0 sends most pairs there, uneven
+    # lengths with n >= 4096 run the length-sorted slots (slot_of in the walk)
+    monkeypatch.setenv("GASALX_TB_BAND_W", w)
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
+    assert "_tbband_" in G.describe_plan(G.make_params(**kw), lens[1], lens[3])
+    b = rand_batch(zlib.crc32(repr((w, n)).encode()) & 0xFFFF, n, *lens)
+    check(engine, no_cigar_overflow(b, **kw), cigar=True, **kw)
+
+
+def test_global_traceback_band_equals_full_matrix(engine, monkeypatch):
+    # config-3 data: the band pass + walk (+ fallback) and the full-matrix flags kernel agree
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
+    b = G.Batch.synth(3, 20000, 0x5EED0003)
+    g1 = engine.align_host(b, G.make_params(**kw))
+    monkeypatch.setenv("GASALX_TB_BAND", "0")
+    assert "_tbband_" not in G.describe_plan(G.make_params(**kw), 300, 300)
+    g0 = engine.align_host(b, G.make_params(**kw))
+    for f in ("score", "n_ops", "cigar"):
+        assert np.array_equal(g0[f], g1[f]), f
+
+
 @pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 3, 5, 2), (1, 1, 0, 1), (3, 6, 0, 0), (5, 4, 10, 1)])
 @pytest.mark.parametrize("alphabet,npen", [(b"ACGT", None), (b"ACGTACGTACGTN", None), (b"ACGTACGTN", 2),
                                            (b"ACGTRY", None)])
