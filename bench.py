@@ -453,6 +453,20 @@ def end_to_end(eng, kind, data, params, cells, reps=5, seed_score=None):
                                      "parameters formed on the device; length-sorted classes)"}
     if kind in (5, 6):
         return res
+    if params.start_pos != G.WITH_TB and not params.is_packed:
+        # the reference's isPacked input (gasal_align.cu:190-201; words as pack_rc_seqs.h:24-31): the
+        # caller's pages hold 4-bit codes, half the bytes move and the kernels read the words
+        # directly; the outputs must equal the ASCII run's
+        pb = dataclasses.replace(data, q_data=pack_host(data.q_data), t_data=pack_host(data.t_data))
+        pp = G.make_params(**{**params_kwargs(params), "is_packed": 1})
+        ref = eng.align_host(data, params, fields=fields, seed_scores=seeds)
+        got = eng.align_host(pb, pp, fields=fields, seed_scores=seeds)
+        bad = sum(int(np.count_nonzero(got[f] != ref[f])) for f in fields)
+        dtk, _ = timed(lambda: eng.align_host(pb, pp, fields=fields, seed_scores=seeds))
+        res["packed_input"] = {"value": round(cells / dtk / 1e9, 2), "ms_per_batch": round(dtk * 1e3, 3),
+                               "h2d_bytes": int((data.q_bytes + data.t_bytes) // 2),
+                               "mismatches_vs_ascii_input": bad,
+                               "path": "gasalx_align_host with isPacked (4-bit words, pageable)"}
     if kind != 5 and params.start_pos == G.WITH_TB:
         host = G.PinnedHost(data.q_bytes)
         dtp, _ = timed(lambda: eng.align_host(data, params, fields=fields, seed_scores=seeds, cigar_out=host.array))
@@ -474,6 +488,25 @@ def end_to_end(eng, kind, data, params, cells, reps=5, seed_score=None):
             if h:
                 h.close()
     return res
+
+
+def pack_host(b):
+    """ASCII bytes -> the reference's packed words (pack_rc_seqs.h:24-31: byte k of each 8 ->
+    nibble at bits 31-4k), returned as bytes padded with zeros to the unpacked length."""
+    nib = (np.asarray(b, np.uint8).reshape(-1, 8) & 0xF).astype(np.uint32)
+    w = np.zeros(nib.shape[0], np.uint32)
+    for k in range(8):
+        w |= nib[:, k] << np.uint32(28 - 4 * k)
+    out = np.zeros(len(b), np.uint8)
+    out[:4 * len(w)] = w.view(np.uint8)
+    return out
+
+
+def params_kwargs(p):
+    return dict(algo=p.algo, start_pos=p.start_pos, second_best=p.second_best, head=p.head, tail=p.tail,
+                match=p.match, mismatch=p.mismatch, gap_open=p.gap_open, gap_extend=p.gap_extend, k_band=p.k_band,
+                n_code=p.n_code, n_penalty=p.n_penalty if p.has_n_penalty else None,
+                max_query_len=p.max_query_len)
 
 
 def dtype_label(plan, kind):

@@ -265,10 +265,13 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         CK(s.meta.reserve(total + 16));
         uint8_t *dm = s.meta.as<uint8_t>();
         uint8_t *p8;
-        if ((rc = stage_in(s.q, hb->q_batch + qlo, qhi - qlo, s.st, &p8))) return rc;
+        // isPacked (score-only): the caller's pages hold 4-bit words, half the bytes of the
+        // unpacked units that offsets and q_bytes count (pack_rc_seqs.h:24-31); only those move
+        const uint64_t pk = params->is_packed ? 2 : 1;
+        if ((rc = stage_in(s.q, hb->q_batch + qlo / pk, (qhi - qlo) / pk, s.st, &p8))) return rc;
         gasalx_batch db = *hb;
         db.q_batch = p8;
-        if ((rc = stage_in(s.t, hb->t_batch + tlo, thi - tlo, s.st, &p8))) return rc;
+        if ((rc = stage_in(s.t, hb->t_batch + tlo / pk, (thi - tlo) / pk, s.st, &p8))) return rc;
         db.t_batch = p8;
         CK(hipMemcpyAsync(dm, h, total, hipMemcpyHostToDevice, s.st));
         db.q_offsets = reinterpret_cast<uint32_t *>(dm + a_qo);
@@ -337,14 +340,18 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     if (chunks_env) n_chunks = (uint32_t)std::max(1, std::atoi(chunks_env));
     const uint32_t chunk = std::max<uint32_t>(16384, (uint32_t)(((uint64_t)n + n_chunks - 1) / n_chunks));
     static const bool single = std::getenv("GASALX_HOST_SINGLE") != nullptr;   // A/B knob
-    if (!single && n >= 2 * chunk && !params->is_packed && contiguous(hb->q_offsets, hb->q_lens, n, hb->q_bytes) &&
+    const bool tb = params->start_pos == 2;
+    if (!single && n >= 2 * chunk && !(params->is_packed && tb) && contiguous(hb->q_offsets, hb->q_lens, n, hb->q_bytes) &&
         contiguous(hb->t_offsets, hb->t_lens, n, hb->t_bytes))
         return align_host_pipelined(eng, params, hb, ho, chunk);
     gasalx_batch db = *hb;
     int rc = 0;
     uint8_t *p8; uint32_t *p32;
-    if ((rc = stage_in(eng->q, hb->q_batch, hb->q_bytes, st, &p8))) return rc; db.q_batch = p8;
-    if ((rc = stage_in(eng->t, hb->t_batch, hb->t_bytes, st, &p8))) return rc; db.t_batch = p8;
+    // isPacked without traceback: only the packed half of the pages moves (with traceback the
+    // device CIGAR buffer starts as the whole query batch, gasal_align.cu:281)
+    const uint32_t pk = params->is_packed && !tb ? 2 : 1;
+    if ((rc = stage_in(eng->q, hb->q_batch, hb->q_bytes / pk, st, &p8))) return rc; db.q_batch = p8;
+    if ((rc = stage_in(eng->t, hb->t_batch, hb->t_bytes / pk, st, &p8))) return rc; db.t_batch = p8;
     if ((rc = stage_in(eng->qo, hb->q_offsets, n, st, &p32))) return rc; db.q_offsets = p32;
     if ((rc = stage_in(eng->to, hb->t_offsets, n, st, &p32))) return rc; db.t_offsets = p32;
     if ((rc = stage_in(eng->ql, hb->q_lens, n, st, &p32))) return rc; db.q_lens = p32;

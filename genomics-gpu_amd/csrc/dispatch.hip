@@ -119,11 +119,11 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
     return nullptr;
 }
 
-static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false) {
+static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false) {
     if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
                                                                      : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
-    return wf16_pick<WF_SEMI>(G, R);
+    return stop ? wf16_pick<WF16_SEMI_STOP>(G, R) : wf16_pick<WF_SEMI>(G, R);
 }
 
 static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
@@ -428,7 +428,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             P16.tbfix = ws.aux.as<int32_t>();
         }
         WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
-                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2);
+                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr);
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -496,6 +496,10 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 // R x wd of every lane's G*R x (ypad) cells (config 3, w = 12: 44 of 304 columns).
 constexpr int WF16_GLOBAL_CP = 7;
 constexpr int WF16_GLOBAL_BAND = 8;
+// SEMI TAIL=TARGET reverse pass of WITH_START (start.hpp, A.stop): the forward instances keep
+// no stop branch, whose per-column constants the compiler hoisted out of the sweep and spilled
+// (config 4: 32 B of scratch per lane, 0.73 GB of traffic per launch)
+constexpr int WF16_SEMI_STOP = 9;
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -529,7 +533,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
-    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : TQ ? WF_SEMI : ALGO_;
+    constexpr bool STOPK = ALGO_ == WF16_SEMI_STOP;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1135,7 +1140,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         uint32_t bestq[2] = {0, 0};                     // TQ: key (H, -row) of the last padded column
         const bool tail_t = !TQ || A.tail == 3;         // the last-row maximum (TAIL TARGET / BOTH)
         int32_t thrp[2] = {0x7FFFFFFF, 0x7FFFFFFF};
-        if (A.stop) {
+        if (STOPK) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (valid[h]) thrp[h] = A.stop[pr[h]] + pb - oe + ge * (int32_t)(yl[h] + G * R);   // its key-frame pattern
@@ -1186,7 +1191,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                             fo -= (uint32_t)ge;
                             const uint32_t cand =
                                 col >= xl[h] ? 0u
-                                : (int32_t)v >= thrp[h]
+                                : STOPK && (int32_t)v >= thrp[h]
                                     ? 0x80000000u | ((255u - (col >> 3)) << 23) | (v << 8) | (255u - (col & 7u))
                                     : (v << 16) | (0xFFFFu - col);
                             best[h] = cand > best[h] ? cand : best[h];

@@ -15,3 +15,7 @@ done
 timeout -k 10 600 python -u -m pytest tests/test_gpu_window_edges.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/edges.log 2>&1
 rc=$?; echo "edges rc=$rc $(tail -1 $O/edges.log)"; [ $rc -eq 0 ] || { tail -30 $O/edges.log; exit $rc; }
 timeout -k 10 120 ./tools/ubench_issue > $O/ubench_issue.json 2> $O/ubench_issue.err; rc=$?; echo "ubench rc=$rc"; cat $O/ubench_issue.json
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "packed_input" > $O/packed.log 2>&1
+rc=$?; echo "packed rc=$rc $(tail -1 $O/packed.log)"; [ $rc -eq 0 ] || { tail -30 $O/packed.log; exit $rc; }
+timeout -k 10 300 python bench.py --workload semi --steps 10 --no-cpu --no-e2e --parity-pairs 200000 > $O/semi.json 2> $O/semi.err
+rc=$?; echo "semi rc=$rc"; python -c "import json; d=json.loads(open('$O/semi.json').read().strip().splitlines()[-1]); print('semi', d['value'], d['ms_per_step'], d['parity']['mismatches'], d['config']['plan'])"

@@ -611,6 +611,28 @@ def test_packed_input(engine):
     assert np.array_equal(g0["score"], g1["score"])
 
 
+@pytest.mark.parametrize("algo,kw", [(G.LOCAL, {}), (G.SEMI_GLOBAL, dict(head=G.TARGET, tail=G.TARGET)),
+                                     (G.GLOBAL, {})])
+def test_packed_input_pipelined_host_path(engine, algo, kw):
+    # isPacked through the two-stream host pipeline (n >= 2 chunks): only the packed half of
+    # the pages moves H2D (capi.cpp); outputs equal the ASCII run's and the oracle's
+    import ctypes
+    b = G.Batch.synth(4 if algo == G.SEMI_GLOBAL else 2, 40000, 0x5EED0002)
+    pq = np.zeros(b.q_bytes // 8, np.uint32)
+    pt = np.zeros(b.t_bytes // 8, np.uint32)
+    O.lib().orc_pack(O._ptr(b.q_data), ctypes.c_uint32(b.q_bytes), O._ptr(pq))
+    O.lib().orc_pack(O._ptr(b.t_data), ctypes.c_uint32(b.t_bytes), O._ptr(pt))
+    qd = np.zeros(b.q_bytes, np.uint8); qd[:b.q_bytes // 2] = pq.view(np.uint8)
+    td = np.zeros(b.t_bytes, np.uint8); td[:b.t_bytes // 2] = pt.view(np.uint8)
+    bp = G.Batch(qd, b.q_offsets, b.q_lens, td, b.t_offsets, b.t_lens)
+    g1 = engine.align_host(bp, G.make_params(algo=algo, is_packed=1, **kw))
+    g0 = engine.align_host(b, G.make_params(algo=algo, **kw))
+    o = O.align(b.slice(0, 4000), O.make_params(algo=algo, **kw))
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(g0[f], g1[f]), f
+        assert np.array_equal(g1[f][:4000], o[f][:4000]), f
+
+
 # ----------------------------------------------------- full-size configs ----
 def test_plan_is_wavefront_for_bench_configs():
     assert G.describe_plan(G.make_params(algo=G.LOCAL), 150, 150).startswith("wavefront16_local")
