@@ -119,14 +119,27 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
     return nullptr;
 }
 
-static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false) {
+static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false) {
     if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
-                                                                     : wf16_pick<WF_LOCAL>(G, R);
+                                                               : ku16 ? wf16_pick<WF16_LOCAL_U16>(G, R)
+                                                                      : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return stop ? wf16_pick<WF16_SEMI_STOP>(G, R) : wf16_pick<WF_SEMI>(G, R);
 }
 
 static inline uint32_t pad8(uint32_t x) { return (x + 7u) & ~7u; }
+
+static bool env_flag(const char *name, bool dflt);
+
+// packed LOCAL with the round-2 keys H*256 + (255 - column): H <= 255, 512 columns (two key
+// sets above 256), 256 with traceback
+static bool local_key16_ok(const gasalx_params &p, uint32_t mq, uint32_t mt) {
+    const int64_t a = p.match, b = p.mismatch, oe = (int64_t)p.gap_open + p.gap_extend;
+    const int64_t k = std::max<int64_t>(b, p.has_n_penalty ? p.n_penalty : 0);
+    const int64_t t8 = pad8(mt);
+    if (a * std::min(mq, mt) > 255 || t8 > (p.start_pos == 2 ? 256 : 512)) return false;
+    return 0x400 + oe + k + 16 + 255 + a + k + 64 <= 0x7BFF;
+}
 
 // The packed kernels (wavefront16.hpp) are exact when every stored value stays
 // inside [0x0400, 0x7BFF] (positive normal f16 patterns) and the score tables
@@ -145,11 +158,13 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
     const int64_t q8 = pad8(mq), t8 = pad8(mt);
     if (wf_algo == WF_LOCAL) {
         const int64_t k = std::max(b, npen);
-        // 16-bit keys H*256 + col: 256 columns each, a second key set up to 512 (not with traceback)
-        if (a + k > 255 || a * std::min(mq, mt) > 255 || t8 > (p.start_pos == 2 ? 256 : 512)) return false;
-        const int64_t base = 0x400 + oe + k + 16;
+        if (a + k > 255) return false;   // table bytes
         *vmin = 0;
-        return base + 255 + a + k + 64 <= 0x7BFF;
+        // 16-bit keys H*256 + col: 256 columns each, a second key set up to 512 (not with traceback)
+        if (local_key16_ok(p, mq, mt)) return true;
+        // the e-drift score kernels key on H*C + col (f16 patterns or u16): make_plan checks
+        // their frame and key range for the chosen shape
+        return p.start_pos != 2 && env_flag("GASALX_KF16", true);
     }
     int64_t k, top, drift = 0;
     if (wf_algo == WF_SEMI) {
@@ -329,18 +344,30 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                                           (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8);
             pl.key2 = wf_algo == WF_LOCAL && y8 > 256;
             // LOCAL score kernels in the e-drift frame (wavefront16.hpp step_local_dr): keys
-            // 0x0400 + H*C + (C-1-c) with C = the padded target length need (Hmax + 1) * C
-            // <= 0x7800; values B + H + e(r + c) over the shape's span stay in the window and
-            // the top lane's first diagonal B - 2e above 0x0400.  GASALX_KF16=0 keeps the
-            // round-2 kernel (A/B runs)
-            if (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && env_flag("GASALX_KF16", true)) {
+            // H*C + (C-1-c) with C = the padded target length, as f16 patterns 0x0400 + key
+            // while (Hmax + 1) * C <= 0x7800, as u16 integers (WF16_LOCAL_U16, one more
+            // instruction per two cells) up to 65536 -- either covers targets past 256 columns
+            // without the second key set; values B + H + e(r + c) over the shape's span stay in
+            // the window and the top lane's first diagonal B - 2e above 0x0400.  GASALX_KF16=0
+            // keeps the round-2 kernel, GASALX_KU16=0 the int32 kernel where only u16 keys fit
+            // (A/B runs)
+            if (wf_algo == WF_LOCAL && !pl.tb && env_flag("GASALX_KF16", true)) {
                 const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
                 const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
                 const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
                 const int64_t span = (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8;
                 const bool frame = base + hmax + e * span + a + k + 64 <= 0x7BFF && base - 2 * e >= 0x400;
-                if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) pl.kf16 = y8;
+                if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) {
+                    pl.kf16 = y8;
+                } else if (frame && (hmax + 1) * (int64_t)y8 <= 0x10000 && y8 <= 0xFFFF &&
+                           env_flag("GASALX_KU16", true)) {
+                    pl.kf16 = y8;
+                    pl.ku16 = true;
+                }
+                if (pl.kf16) pl.key2 = false;
             }
+            // outside both frames the round-2 keys must hold (packed16_ok admitted the drift case)
+            if (wf_algo == WF_LOCAL && !pl.kf16 && !local_key16_ok(p, s.max_q, s.max_t)) pl.packed16 = false;
             pl.semi_tq = pl.semi_tq && pl.packed16;
             // GLOBAL + traceback: the score sweep stores band checkpoints, a second pass
             // recomputes each lane's band window with flags, the walk leaves the band only
@@ -362,7 +389,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             // (_nodrift: a LOCAL score plan outside the e-drift frame's window, the round-2 kernel)
             pl.name = std::string("wavefront16_") + an + (pl.tb ? (pl.tb_band ? "_tbband" : "_tb") : "") +
                       (pl.key2 ? "_k2" : "") +
-                      (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && !pl.kf16 ? "_nodrift" : "") + "_G" +
+                      (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && !pl.kf16 ? "_nodrift" : "") +
+                      (pl.ku16 ? "_u16" : "") + "_G" +
                       std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
         else
             pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
@@ -428,7 +456,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             P16.tbfix = ws.aux.as<int32_t>();
         }
         WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
-                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr);
+                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16);
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -59,6 +59,7 @@ struct Plan {
     size_t lds16_bytes = 0;
     int32_t vmin = 0;       // packed GLOBAL/SEMI value-range bound
     uint32_t kf16 = 0;      // packed LOCAL: f16-pattern key columns (wavefront16.hpp step_local KU), 0 = 16-bit keys
+    bool ku16 = false;      // packed LOCAL in the e-drift frame with u16 keys (WF16_LOCAL_U16)
     int G = 0, R = 0;
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;

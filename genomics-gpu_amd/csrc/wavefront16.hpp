@@ -208,7 +208,11 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
 // FL - 2e (borrow-free 32-bit subtracts: Hin = H^(r, c) >= FL - 2e, H >= FL - e),
 // two columns per v_pk_maximum3 (KEYS: the second step of a pair).
 // ---------------------------------------------------------------------------
-template <int R, bool KEYS>
+// U16 (WF16_LOCAL_U16 launches): the keys are plain u16 integers H*C + (C-1-c), ordered by
+// two v_pk_max_u16 instead of one f16-pattern v_pk_maximum3 (one instruction more per two
+// cells), so (Hmax + 1) * C may reach 65536 instead of 0x7800: 150 bp at match 2, where the
+// round-3 planner fell back to the int32 kernel (2,627 GCUPS)
+template <int R, bool KEYS, bool U16 = false>
 __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                               const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                               uint32_t (&Ek)[R], uint32_t (&key)[R], uint32_t (&FL)[R],
@@ -228,7 +232,10 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
             // 32-bit subtracts, borrow-free: Hin >= FL - 2e and H >= FL - e
             const uint32_t g2 = pk_subnb(FL[k], EXT2);
             const uint32_t d1 = pk_subnb(Hin[k], g2), d2 = pk_subnb(H, g2);
-            key[k] = pk_max3(key[k], pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn));
+            if (U16)
+                key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn)));
+            else
+                key[k] = pk_max3(key[k], pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn));
         }
         FL[k] = pk_addnc(FL[k], EXT);
         f = pk_max_u16(toe, f);
@@ -500,6 +507,7 @@ constexpr int WF16_GLOBAL_BAND = 8;
 // no stop branch, whose per-column constants the compiler hoisted out of the sweep and spilled
 // (config 4: 32 B of scratch per lane, 0.73 GB of traffic per launch)
 constexpr int WF16_SEMI_STOP = 9;
+constexpr int WF16_LOCAL_U16 = 10;    // LOCAL score + ends in the e-drift frame, u16 keys (step_local_dr U16)
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -529,12 +537,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     constexpr bool GT = GTB || GCP || GBD;   // the traceback kernels' declines and start-cell capture
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
+    constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16;
     // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
     constexpr bool STOPK = ALGO_ == WF16_SEMI_STOP;
-    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -805,9 +814,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 const uint32_t EXT2 = pk_bcast(2 * ge);
                 const uint32_t KXD = (uint32_t)((P.k - 2 * ge) * 0x10001),
                                OEXD = (uint32_t)((P.k - 2 * ge + A.o) * 0x10001);
+                constexpr uint32_t KOFS = KU16 ? 0u : 0x0400u;   // u16 keys need no f16 offset
                 auto inv = [&](int32_t cc, uint32_t add) {
                     const uint32_t term = (cc >= 0 && (uint32_t)cc < C) ? C - 1u - (uint32_t)cc : 0u;
-                    return ((0x0400u + term + add * C) & 0xFFFFu) * 0x10001u;
+                    return ((KOFS + term + add * C) & 0xFFFFu) * 0x10001u;
                 };
                 // Each lane keeps the frame shifted by its own constant, e(k + s) instead of
                 // e(r + c) (r = lg*R + k, c = s - lg): every floor FL[k] = B + e(k + s + 1) is
@@ -816,7 +826,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 uint32_t FL[R];
 #pragma unroll
                 for (int k = 0; k < R; ++k) {
-                    key[k] = 0x04000400u;
+                    key[k] = KOFS * 0x10001u;
                     HA[k] = (uint32_t)(pbv + ge * (k - 1)) * 0x10001u;   // H^(r, c0 - 1) = 0
                     Ek[k] = (uint32_t)(pbv + ge * k) * 0x10001u;         // E^(r, c0) = its floor
                     FL[k] = (uint32_t)(pbv + ge * (k + 1)) * 0x10001u;   // floor of E(r, c0 + 1)
@@ -830,7 +840,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     uint2 T = tnext;
                     tnext = tcol[c + 1 + G];
                     const uint32_t dt0 = (uint32_t)(pbv + ge * (c - 2)) * 0x10001u;   // lane 0: H^(-1, c - 1)
-                    step_local_dr<R, false>(T, top ? dt0 : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, FL, f,
+                    step_local_dr<R, false, KU16>(T, top ? dt0 : prevRecvH, top ? BB : recvF, xs, HA, HB, Ek, key, FL, f,
                                             KXD, OEXD, EXT, KMC, 0u, 0u, EXT2);
                     prevRecvH = recvH;
                     recvH = pk_subnb((uint32_t)shr_lane((int32_t)HB[R - 1]), ADJ);
@@ -838,7 +848,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     T = tnext;
                     tnext = tcol[c + 2 + G];
                     const uint32_t dt1 = (uint32_t)(pbv + ge * (c - 1)) * 0x10001u;
-                    step_local_dr<R, true>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
+                    step_local_dr<R, true, KU16>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
                                            KXD, OEXD, EXT, KMC, inv(c, 0), inv(c + 1, (uint32_t)(-ge)), EXT2);
                     prevRecvH = recvH;
                     recvH = pk_subnb((uint32_t)shr_lane((int32_t)HA[R - 1]), ADJ);
@@ -857,8 +867,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 const uint32_t r = r0 + k;
                 const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
                 uint32_t H = kk >> 8, col = 255u - (kk & 0xFFu);
-                if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c)
-                    const uint32_t C = A.kf16, x = kk - 0x0400u;
+                if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c) (u16 keys: no 0x0400)
+                    const uint32_t C = A.kf16, x = kk - (KU16 ? 0u : 0x0400u);
                     H = x / C;
                     col = C - 1u - (x - H * C);
                 }

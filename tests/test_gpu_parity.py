@@ -698,7 +698,7 @@ def test_local_packed_mixed_lengths_and_n(engine):
 
 
 def test_local_packed_vs_int32_paths_agree(engine):
-    # match=1 uses the packed kernel; the same scores scaled by 2 use the int32 one
+    # match=1 uses the f16-key packed kernel; the same scores scaled by 2 the u16-key one
     b = G.Batch.synth(2, 5000, 7)
     r1 = engine.align_host(b, G.make_params(algo=G.LOCAL))
     r2 = engine.align_host(b, G.make_params(algo=G.LOCAL, match=2, mismatch=8, gap_open=12, gap_extend=2))

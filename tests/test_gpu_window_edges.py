@@ -113,8 +113,42 @@ def test_local_drift_frame_length_edge(engine, scores):
     inside = edge_batch(_seed(scores, 0), 600, L)
     check(engine, inside, kw)
     past = plan(kw, L + 8, L + 8)
-    assert past.startswith(("wavefront16_local_nodrift_G", "wavefront_local")), past
+    assert past.startswith(("wavefront16_local_u16_G", "wavefront16_local_nodrift_G", "wavefront_local")), past
     check(engine, edge_batch(_seed(scores, 1), 600, L + 8), kw)
+
+
+@pytest.mark.parametrize("scores", [(1, 4, 6, 1), (2, 4, 6, 1), (2, 3, 5, 2)])
+def test_local_u16_key_length_edge(engine, scores):
+    # u16 keys (WF16_LOCAL_U16): (Hmax + 1) * C <= 65536; the first length past it takes the
+    # round-2 kernel or the int32 one
+    a, b, o, e = scores
+    kw = dict(algo=G.LOCAL, match=a, mismatch=b, gap_open=o, gap_extend=e)
+    L = None
+    for cand in range(16, 600, 8):
+        if plan(kw, cand, cand).startswith("wavefront16_local_u16_G"):
+            L = cand
+        elif L is not None:
+            break
+    assert L is not None
+    check(engine, edge_batch(_seed("u16", scores, 0), 600, L), kw)
+    past = plan(kw, L + 8, L + 8)
+    assert not past.startswith("wavefront16_local_u16_G"), past
+    check(engine, edge_batch(_seed("u16", scores, 1), 300, L + 8), kw)
+
+
+def test_local_u16_keys_config2_match2_and_long_targets(engine):
+    # config 2 at match 2 (outside the round-2 window) and 150 x 400 pairs (u16 keys instead
+    # of the second key set), score + ends and WITH_START
+    b = G.Batch.synth(2, 20000, 0x5EED0002)
+    kw = dict(algo=G.LOCAL, match=2)
+    assert plan(kw, 150, 150).startswith("wavefront16_local_u16_G")
+    check(engine, b, kw)
+    check(engine, b.slice(0, 6000), dict(kw, start_pos=G.WITH_START))
+    rng = np.random.default_rng(77)
+    qs, ts = helpers.random_pairs(rng, 3000, 100, 150, 200, 400)
+    b2 = G.Batch.from_pairs(qs, ts)
+    assert plan(dict(algo=G.LOCAL), 150, 400).startswith("wavefront16_local_u16_G")
+    check(engine, b2, dict(algo=G.LOCAL))
 
 
 @pytest.mark.parametrize("L", [40, 150])
