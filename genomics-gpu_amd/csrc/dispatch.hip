@@ -119,10 +119,11 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
     return nullptr;
 }
 
-static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false) {
+static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false,
+                        bool lrs = false) {
     if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
-                                                               : ku16 ? wf16_pick<WF16_LOCAL_U16>(G, R)
-                                                                      : wf16_pick<WF_LOCAL>(G, R);
+                                                               : (ku16 || lrs) ? wf16_local_lookup(G, R, ku16, lrs)
+                                                                               : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return stop ? wf16_pick<WF16_SEMI_STOP>(G, R) : wf16_pick<WF_SEMI>(G, R);
 }
@@ -456,7 +457,8 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             P16.tbfix = ws.aux.as<int32_t>();
         }
         WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
-                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16);
+                              : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16,
+                                            A.lstop != nullptr && pl.kf16 != 0);
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -586,16 +588,21 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     const size_t sh = (size_t)(t8w + 1) * 4;
     if (2 * sh > 64 * 1024) { set_error("WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
     HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist);
+    // LOCAL: slots that stop early (the drift sweep's lstop) share waves (start.hpp rev_bucket);
+    // GASALX_START_STOP=0 keeps the full reverse rectangle and the length order (A/B)
+    const bool lstop = mode == REV_LOCAL && env_flag("GASALX_START_STOP", true);
+    const int32_t *skey = lstop ? score : nullptr;
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match);
     rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
-    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm);
+    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm, nullptr,
+                                                              skey, p.match);
     HIPCHK(hipGetLastError());
     RevArgs R;
     R.q = q; R.t = t; R.qoff = b.q_offsets; R.toff = b.t_offsets; R.qlen = b.q_lens; R.tlen = b.t_lens;
     R.qend = qend; R.tend = tend; R.score = score;
     R.rq = ws.rev_q.as<uint8_t>(); R.rt = ws.rev_t.as<uint8_t>();
     R.rqoff = meta; R.rtoff = meta + n; R.rqlen = meta + 2 * (size_t)n; R.rtlen = meta + 3 * (size_t)n;
-    R.stop = mode == REV_SEMI ? stop : nullptr;
+    R.stop = (mode == REV_SEMI || lstop) ? stop : nullptr;   // the forward score per slot
     R.n = n; R.q8w = q8 / 8; R.t8w = t8w; R.packed = packed; R.mode = mode;
     R.fill = 0x01010101u * (uint32_t)(p.n_code & 0xFF);
     R.nval = (uint32_t)(p.n_code & 0xF);
@@ -613,7 +620,8 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     A.q = R.rq; A.t = R.rt;
     A.qoff = R.rqoff; A.toff = R.rtoff; A.qlen = R.rqlen; A.tlen = R.rtlen;
     A.score = rscore; A.qend = rqend; A.tend = rtend;
-    A.stop = R.stop;
+    A.stop = mode == REV_SEMI ? R.stop : nullptr;
+    A.lstop = lstop ? R.stop : nullptr;
     A.n = n;
     A.packed = 0;
     int rc = launch_wavefront(ws, pl, pr, A, st);

@@ -130,18 +130,29 @@ __device__ __forceinline__ uint2 rev_first(const uint8_t *seq, uint32_t off, uin
     return make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24), b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
 }
 
+// sort key of the reverse pass's slots: the reversed target length, or (LOCAL with the forward
+// scores, whose sweep stops once the score is reached) the shorter of it and a span estimate of
+// the alignment, 2 * ceil(score / match) + 16 columns -- a wave's step count is set by its
+// slowest pair, so pairs that will stop early share waves (a heuristic: the results do not
+// depend on the order)
 __device__ __forceinline__ uint32_t rev_bucket(int32_t mode, const uint32_t *tlen, const int32_t *tend, uint32_t k,
-                                               uint32_t t8w) {
-    return t8w - min((rev_tlen(mode, tlen, tend, k) + 7) >> 3, t8w);   // 0 = longest
+                                               uint32_t t8w, const int32_t *score = nullptr, int32_t a = 1) {
+    uint32_t L = rev_tlen(mode, tlen, tend, k);
+    if (score && mode == REV_LOCAL && a > 0) {
+        const int32_t sc = max(score[k], 0);
+        L = min(L, (uint32_t)(2 * ((sc + a - 1) / a) + 16));
+    }
+    return t8w - min((L + 7) >> 3, t8w);   // 0 = longest
 }
 
 __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
-                                                       uint32_t n, uint32_t t8w, uint32_t *hist) {
+                                                       uint32_t n, uint32_t t8w, uint32_t *hist,
+                                                       const int32_t *score = nullptr, int32_t a = 1) {
     extern __shared__ uint32_t cnt[];   // t8w + 1 buckets
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) atomicAdd(&cnt[rev_bucket(mode, tlen, tend, k, t8w)], 1u);
+    if (k < n) atomicAdd(&cnt[rev_bucket(mode, tlen, tend, k, t8w, score, a)], 1u);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
         if (cnt[i]) atomicAdd(&hist[i], cnt[i]);
@@ -166,14 +177,15 @@ __global__ __launch_bounds__(256) void rev_scan_kernel(const uint32_t *hist, uin
 
 __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                           uint32_t n, uint32_t t8w, uint32_t *cursor,
-                                                          uint32_t *perm, uint32_t *inv = nullptr) {
+                                                          uint32_t *perm, uint32_t *inv = nullptr,
+                                                          const int32_t *score = nullptr, int32_t a = 1) {
     extern __shared__ uint32_t cnt[];   // [t8w+1] counts, then [t8w+1] bases
     uint32_t *base = cnt + t8w + 1;
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t b = 0, local = 0;
-    if (k < n) { b = rev_bucket(mode, tlen, tend, k, t8w); local = atomicAdd(&cnt[b], 1u); }
+    if (k < n) { b = rev_bucket(mode, tlen, tend, k, t8w, score, a); local = atomicAdd(&cnt[b], 1u); }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
         if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);

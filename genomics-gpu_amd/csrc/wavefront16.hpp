@@ -113,6 +113,16 @@ __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
     return (uint32_t)(((lut | set) >> (4 * (nib & 15u))) & 15u);
 }
 
+// every G-lane group of a wave ballot has a bit set
+template <int G>
+__device__ __forceinline__ bool groups_all(uint64_t b) {
+    constexpr uint64_t low = G == 64 ? 1ull : G == 32 ? 0x0000000100000001ull : G == 16 ? 0x0001000100010001ull
+                                                                                      : 0x0101010101010101ull;
+#pragma unroll
+    for (int sh = 1; sh < G; sh <<= 1) b |= b >> sh;
+    return (b & low) == low;
+}
+
 // Value-range constants of one launch (dispatch.hip packed16_ok checks that the
 // stored values stay inside [0x0400, 0x7BFF] for these).
 struct Pk16 {
@@ -508,6 +518,8 @@ constexpr int WF16_GLOBAL_BAND = 8;
 // (config 4: 32 B of scratch per lane, 0.73 GB of traffic per launch)
 constexpr int WF16_SEMI_STOP = 9;
 constexpr int WF16_LOCAL_U16 = 10;    // LOCAL score + ends in the e-drift frame, u16 keys (step_local_dr U16)
+constexpr int WF16_LOCAL_RS = 11;     // LOCAL reverse pass of WITH_START (A.lstop early stop), f16 keys
+constexpr int WF16_LOCAL_U16_RS = 12; // the same with u16 keys (local_rs.hip instances)
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -537,13 +549,14 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     constexpr bool GT = GTB || GCP || GBD;   // the traceback kernels' declines and start-cell capture
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
-    constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16;
+    constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16 || ALGO_ == WF16_LOCAL_U16_RS;
+    constexpr bool LRS = ALGO_ == WF16_LOCAL_RS || ALGO_ == WF16_LOCAL_U16_RS;   // (the check costs VGPRs)
     // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
     constexpr bool STOPK = ALGO_ == WF16_SEMI_STOP;
-    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16 || LRS) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -836,6 +849,16 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // (lane 1's upper lane has no garbage column -1): H = 0 at k = -1, s - 1
                 prevRecvH = (uint32_t)(pbv - 2 * ge) * 0x10001u;
                 recvH = (uint32_t)(pbv - ge) * 0x10001u;
+                // WITH_START reverse pass (A.lstop, start.hpp): no cell exceeds the forward score
+                // S, so a key >= KOFS + S*C + (C-1-m) is a cell reaching S in a column <= m.  Once
+                // lane G-1 has finished the strips up to column m and every pair has such a cell,
+                // its first one in strip-major order (Q1) is settled: the sweep stops there
+                // (local_kernel_template.h:441-511 stops at the first cell reaching the score).
+                int32_t sstop[2] = {0, 0};
+                if (LRS) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) sstop[h] = valid[h] ? A.lstop[pr[h]] : 0;
+                }
                 for (; s < nsteps; s += 2, c += 2) {
                     uint2 T = tnext;
                     tnext = tcol[c + 1 + G];
@@ -853,6 +876,22 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     prevRecvH = recvH;
                     recvH = pk_subnb((uint32_t)shr_lane((int32_t)HA[R - 1]), ADJ);
                     recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
+                    if (LRS && (s & 7u) == 6u) {
+                        const int32_t cl = (int32_t)s + 1 - (G - 1);                // lane G-1's last column
+                        const int32_t m = min(((cl + 1) & ~7) - 1, (int32_t)C - 1);   // last settled strip's end
+                        if (m >= 0) {
+                            uint32_t mx = key[0];
+#pragma unroll
+                            for (int k = 1; k < R; ++k) mx = pk_max_u16(mx, key[k]);
+                            bool hit[2];
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const uint32_t thr = KOFS + (uint32_t)sstop[h] * C + (C - 1u - (uint32_t)m);
+                                hit[h] = !valid[h] || sstop[h] <= 0 || ((mx >> (16 * h)) & 0xFFFFu) >= thr;
+                            }
+                            if (groups_all<G>(__ballot(hit[0])) && groups_all<G>(__ballot(hit[1]))) break;
+                        }
+                    }
                 }
             } else {
                 sweep(std::integral_constant<int, 0>{}, nsteps);
@@ -1254,5 +1293,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 // length 8R): NULL outside that range
 using Wf16Fn = void (*)(WfArgs);
 Wf16Fn wf16_tq_lookup(int R);
+// LOCAL e-drift instances with u16 keys and/or the reverse pass's early stop (local_rs.hip):
+// NULL for shapes outside kShapes16
+Wf16Fn wf16_local_lookup(int G, int R, bool u16, bool rs);
 
 }  // namespace gx
