@@ -43,9 +43,12 @@ import gasal_ffi as G  # noqa: E402
 import gasal_dist as D  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU lane throughput: 256 CUs x 4 SIMDs x 16 lanes per clock x 2.4 GHz
-VALU_LANE_OPS = 256 * 4 * 16 * 2.4e9            # 39.3 T int32 (or fp32) ops/s
 SIMDS, CLOCK = 256 * 4, 2.4e9
+# VALU lane throughput, MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction every 2 cycles per
+# SIMD -> 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz = 78.6 T 32-bit lane-ops/s; the FP32 vector peak
+# counts an FMA as 2 flops: 157.3 TFLOPS
+VALU_LANE_OPS = SIMDS * 32 * CLOCK
+FP32_VECTOR_PEAK = 2 * VALU_LANE_OPS            # 157.3 TFLOPS (MI355X_MICROARCH.md MFMA table, F32 row)
 
 MAIN_METRIC = "GCUPS on batched 150bp affine-gap SW at 1/2/4/8 MI355X; HBM-roofline %"
 
@@ -901,49 +904,49 @@ def main():
         same = (pmc is not None and pmc.get("pairs_per_launch") == n and pmc.get("plan") == plan and
                 pmc.get("lib_sha256") == sha and not probe)
         traffic = pmc.get("hbm_bytes_per_launch") if same else None
-        packed = plan.startswith(("wavefront16", "nvbio16")) or wl.get("packed", False)
-        lane_rate = VALU_LANE_OPS * (2 if packed else 1)
         kcells = cells_per_step / kern_s
+        # VALU roofline of the dominant kernel: its own wave-instructions (PMC SQ_INSTS_VALU of a
+        # pass over this very library and plan) issued back to back at the SIMD's full rate -- one
+        # wave64 instruction per 2 cycles per SIMD-32 (MI355X_MICROARCH.md), 1,024 SIMDs at 2.4
+        # GHz -- is the fastest that instruction stream can run, so frac = that time / the
+        # measured time <= 1.  Instructions priced above 2 cycles (VOP3P, v_perm, FMA: the
+        # measured table profiles/r04_valu_issue_rates.json) keep frac below 1 at full issue.
+        # Without a matching PMC file peak and frac stay null; the SURVEY 8(d) algorithmic op
+        # count is reported as a rate beside it, not as a fraction (the packed kernels issue
+        # fewer instructions than it counts).
+        valu = {"bound": "valu issue", "achieved": round(kcells / 1e12, 4), "unit": "T cells/s",
+                "peak": None, "frac": None,
+                "basis": "the kernel's VALU wave-instructions per cell (PMC SQ_INSTS_VALU) at one per 2 cycles "
+                         "per SIMD-32 (MI355X_MICROARCH.md), 1,024 SIMDs x 2.4 GHz"}
+        if kind == 6 or wl["ops"] is None:
+            bcells = band_cells_of(data, pkw.get("k_band", 0)) if kind != 6 else cells_per_step
+            if kind != 6:
+                valu["band_cells_per_step"] = bcells
+                valu["band_fraction"] = round(bcells / cells_per_step, 4)
+        ops = wl["ops"] or 12
+        valu["algorithmic"] = {"ops_per_cell": ops, "achieved_t_ops": round(kcells * ops / 1e12, 3),
+                               "basis": "SURVEY.md 8(d) algorithmic ops per cell (informational: a rate, not a "
+                                        "fraction of the VALU ceiling)"}
         if kind == 5:
-            # fp32 flops (an FMA counts 2) at the non-packed fp32 VALU rate, 78.6 TFLOPS; packed
-            # v_pk_fma_f32 measured no faster here (profiles/r02_pairhmm_ab.md)
-            peak_cells = 2 * VALU_LANE_OPS / wl["ops"]
-            valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
-                    "unit": "T cells/s", "frac": round(kcells / peak_cells, 4), "ops_per_cell": wl["ops"],
-                    "basis": "SURVEY.md 8(d): 11 fp32 flops per cell (3 FMA = 6, 4 mul, 1 add) at the non-packed "
-                             "fp32 VALU rate 78.6 TFLOPS"}
-        elif wl["ops"]:
-            peak_cells = lane_rate / wl["ops"]
-            valu = {"bound": "valu", "achieved": round(kcells / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
-                    "unit": "T cells/s", "frac": round(kcells / peak_cells, 4), "ops_per_cell": wl["ops"],
-                    "basis": (f"SURVEY.md 8(d) algorithmic ops per cell (11 for semi-global: H-based Gotoh, "
-                              f"no per-cell running max) at {'packed 2x16-bit / 2xfp32' if packed else 'int32'} "
-                              f"VALU lane rate {lane_rate / 1e12:.1f} T ops/s")}
-        else:
-            # banded: GCUPS counts the full rectangle (the metric's cells); the kernel
-            # computes the tiles of the band only, so its roofline is over those
-            bcells = band_cells_of(data, pkw.get("k_band", 0))
-            bk = bcells / kern_s
-            rate = VALU_LANE_OPS * (2 if plan.startswith("banded16") else 1)
-            peak_cells = rate / 12
-            valu = {"bound": "valu", "achieved": round(bk / 1e12, 4), "peak": round(peak_cells / 1e12, 4),
-                    "unit": "T cells/s (cells of the band)", "frac": round(bk / peak_cells, 4), "ops_per_cell": 12,
-                    "band_cells_per_step": bcells, "band_fraction": round(bcells / cells_per_step, 4),
-                    "basis": "SURVEY.md 8(d) 12 algorithmic ops per local cell over the cells of the band "
-                             "(banded.h:35,73-75) at the " + ("packed 2x16-bit" if rate > VALU_LANE_OPS else "int32") +
-                             f" VALU lane rate {rate / 1e12:.1f} T ops/s"}
+            fl = kcells * wl["ops"]
+            valu["fp32"] = {"achieved_tflops": round(fl / 1e12, 2), "peak_tflops": round(FP32_VECTOR_PEAK / 1e12, 1),
+                            "frac": round(fl / FP32_VECTOR_PEAK, 4),
+                            "basis": "11 fp32 flops per cell (3 FMA = 6, 4 mul, 1 add; SURVEY.md 8(d)) against "
+                                     "the FP32 vector peak 157.3 TFLOPS (MI355X_MICROARCH.md)"}
         if same and pmc.get("valu_insts_per_launch"):
-            # issue-slot use: VALU issue cycles of the dominant kernel (SQ_ACTIVE_INST_VALU counts
-            # quad-cycles, MI355X_MICROARCH.md) over the SIMD-cycles of its launch at 2.4 GHz
             pk_t = pmc.get("kernel_ns", 0) / 1e9 or kern_s
-            act = pmc.get("counters", {}).get("SQ_ACTIVE_INST_VALU")
-            valu["issue"] = {"valu_wave_instr_per_launch": pmc["valu_insts_per_launch"],
-                             "cycles_per_valu_instr_per_simd":
-                                 round(SIMDS * CLOCK * pk_t / pmc["valu_insts_per_launch"], 3),
-                             "issue_slot_use": round(4 * act / (SIMDS * CLOCK * pk_t), 4) if act else None,
-                             "kernel": pmc.get("kernel"),
-                             "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU; "
-                                       f"same library sha256 and plan as this run)"}
+            vi = float(pmc["valu_insts_per_launch"])
+            cells_launch = bcells if (wl["ops"] is None and kind != 6) else cells_per_step
+            t_issue = vi * 2.0 / (SIMDS * CLOCK)            # every instruction at the full rate
+            peak_cells = cells_launch / t_issue
+            ach = cells_launch / pk_t
+            valu.update({"peak": round(peak_cells / 1e12, 4), "achieved": round(ach / 1e12, 4),
+                         "frac": round(ach / peak_cells, 4),
+                         "instr_per_cell": round(vi * 64 / cells_launch, 3),
+                         "cycles_per_instr_per_simd": round(SIMDS * CLOCK * pk_t / vi, 3),
+                         "kernel": pmc.get("kernel"), "kernel_ms_pmc": round(pk_t * 1e3, 4),
+                         "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU; same library sha256 and "
+                                   f"plan as this run)"})
         out = {
             "metric": METRICS.get(args.workload, MAIN_METRIC),
             "value": round(gcups, 2),

@@ -80,9 +80,6 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #ifndef GX_PROBE_LOCAL
 #define GX_PROBE_LOCAL 0   // step_local timing probes (bit 0: F, bit 1: E without the extension subtract)
 #endif
-#ifndef GX_WF16_CAPTURE_TREE
-#define GX_WF16_CAPTURE_TREE 0   // GLOBAL kernels: branch-free score / start-cell capture
-#endif
 #ifndef GX_WF16_TB_INPLACE
 #define GX_WF16_TB_INPLACE 0
 #endif
@@ -955,9 +952,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         uint32_t kq_lane[2], kq[2], kp_lane[2], kp[2];
         bool fixable[2];
         int32_t score[2] = {0, 0}, fixv[2] = {0, 0};
-#if GX_WF16_CAPTURE_TREE
-        uint32_t capq[2] = {0, 0}, capp[2] = {0, 0};   // the captured registers
-#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             kq_lane[h] = (xl[h] - 1) / R;
@@ -980,10 +974,37 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         uint32_t *cpw = GCP ? A.cp + ((size_t)wv * 64 + lane) * (2 * R) : nullptr;   // [wave][lane][2R]
         uint2 *stw = GCP ? A.stm + (size_t)wv * (A.band_wd + 1) * 64 + lane : nullptr;
         uint2 tnext = tcol[c + G];
-        auto half_step = [&](const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+        // Capture window: the steps at which some lane of the wave holds a cell to capture --
+        // row xl - 1 at column yl - 1 (the score, global.h:98-103,299) and, for traceback, row
+        // xl at column yl (the start cell, tb_kernel) -- so that the steps outside it carry no
+        // capture code: its per-register selects, if-converted, ran on every step (597 VALU
+        // instructions per two steps of G16R20 instead of ~300, kernel_census.py).
+        uint32_t cap_lo = 0xFFFFFFFFu, cap_hi = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (valid[h]) {
+                const uint32_t sq = yl[h] - 1 + kq_lane[h];
+                cap_lo = min(cap_lo, sq);
+                cap_hi = max(cap_hi, sq);
+                if (fixable[h]) {
+                    const uint32_t sf = yl[h] + kp_lane[h];
+                    cap_lo = min(cap_lo, sf);
+                    cap_hi = max(cap_hi, sf);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+            cap_lo = min(cap_lo, (uint32_t)__shfl_xor(cap_lo, m));
+            cap_hi = max(cap_hi, (uint32_t)__shfl_xor(cap_hi, m));
+        }
+        // FLG bit 0: a lane may reach column -1 (its reset to the left boundary) in this
+        // phase; bit 1: captures
+        auto half_step = [&](auto flg, const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+            constexpr int FLG = decltype(flg)::value;
             const uint2 T = tnext;
             tnext = tcol[cc + 1 + G];
-            if (cc == -1) {
+            if ((FLG & 1) && cc == -1) {
                 int32_t rr = (int32_t)r0;
                 asm volatile("" : "+v"(rr));   // keep the R boundary values out of loop-invariant registers
 #pragma unroll
@@ -1001,46 +1022,24 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                       OEX, NN, j);
                 else
                     step_global<R, GCP>(T, top ? dtop : prevRecvH, top ? NN : recvF, xs, Hin, Hout, Ek, f, KX, OEX, NN);
-#if GX_WF16_CAPTURE_TREE
-                // branch-free capture: every lane picks one register by a select tree
-                // over the bits of its index (score: row xl - 1 at column yl - 1; fix:
-                // row xl at column yl); a capture inside a per-lane branch holds ~45
-                // more VGPRs
+                if constexpr ((FLG & 2) != 0) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const bool late = GT && cc >= (int32_t)yl[h];
-                    const uint32_t idx = late ? kp[h] : kq[h];
-                    uint32_t t[R];
+                    for (int h = 0; h < 2; ++h) {
+                        if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
+                            uint32_t v = 0;
 #pragma unroll
-                    for (int k = 0; k < R; ++k) t[k] = Hout[k];
+                            for (int k = 0; k < R; ++k) v = (k == (int)kq[h]) ? Hout[k] : v;
+                            score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h] - 2);
+                        }
+                        if (fixable[h] && cc == (int32_t)yl[h] && lg == kp_lane[h]) {
+                            uint32_t v = 0;
 #pragma unroll
-                    for (int bb = 1; bb < R; bb <<= 1) {
-                        const bool bit = (idx & (uint32_t)bb) != 0;
-#pragma unroll
-                        for (int k = 0; k + bb < R; k += 2 * bb) t[k] = bit ? t[k + bb] : t[k];
-                    }
-                    capq[h] = cc == (int32_t)yl[h] - 1 ? t[0] : capq[h];
-                    if (GT) capp[h] = cc == (int32_t)yl[h] ? t[0] : capp[h];
-                }
-            }
-#else
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    if (valid[h] && cc == (int32_t)yl[h] - 1 && lg == kq_lane[h]) {   // global.h:98-103,299
-                        uint32_t v = 0;
-#pragma unroll
-                        for (int k = 0; k < R; ++k) v = (k == (int)kq[h]) ? Hout[k] : v;
-                        score[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h] - 2);
-                    }
-                    if (fixable[h] && cc == (int32_t)yl[h] && lg == kp_lane[h]) {
-                        uint32_t v = 0;
-#pragma unroll
-                        for (int k = 0; k < R; ++k) v = (k == (int)kp[h]) ? Hout[k] : v;
-                        fixv[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
+                            for (int k = 0; k < R; ++k) v = (k == (int)kp[h]) ? Hout[k] : v;
+                            fixv[h] = (int32_t)((v >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
+                        }
                     }
                 }
             }
-#endif
             if constexpr (GCP) {
                 if (cp_on && cc == cs_own) {
 #pragma unroll
@@ -1056,92 +1055,45 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
             recvF = (uint32_t)shr_lane((int32_t)f);
         };
-        if constexpr (GTB) {
-            // Direction flags, skewed layout (read by tb_kernel): windows w = (column +
-            // lane) / 4 holding the 4-step window's flags, every lane stores after the
-            // same steps (tb_store_window: per pair, or 8 pairs interleaved).
-            static_assert(R % 4 == 0, "GLOBAL+TB packed shapes need R % 4 == 0");
-            uint32_t W16[2];
+        // Direction flags (GTB), skewed layout (read by tb_kernel): windows w = (column + lane)
+        // / 4 holding the 4-step window's flags, every lane stores after the same steps
+        // (tb_store_window: per pair, or 8 pairs interleaved).
+        static_assert(!GTB || R % 4 == 0, "GLOBAL+TB packed shapes need R % 4 == 0");
+        uint32_t W16[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
-            for (uint32_t s = 0; s < nsteps; s += 4, c += 4) {
-#if GX_WF16_TB_INPLACE
-                // one H array updated in place (each row reads its old H as the next
-                // row's diagonal before writing the new one): R fewer live VGPRs
-                half_step(c, 0, HA, HA);
-                half_step(c + 1, 1, HA, HA);
-                half_step(c + 2, 2, HA, HA);
-                half_step(c + 3, 3, HA, HA);
-#else
-                half_step(c, 0, HA, HB);
-                half_step(c + 1, 1, HB, HA);
-                half_step(c + 2, 2, HA, HB);
-                half_step(c + 3, 3, HB, HA);
-#endif
-                const uint32_t w = s >> 2;
+        for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
+        constexpr uint32_t STEP = GTB ? 4 : 2;
+        uint32_t s = 0;
+        auto run = [&](auto flg, const uint32_t end) {
+            for (; s < end; s += STEP, c += STEP) {
+                if constexpr (GTB) {
+                    half_step(flg, c, 0, HA, HB);
+                    half_step(flg, c + 1, 1, HB, HA);
+                    half_step(flg, c + 2, 2, HA, HB);
+                    half_step(flg, c + 3, 3, HB, HA);
 #if GX_TB_STORE_MODE == 1
-                // timing probe only: no direction stores (results invalid)
-                asm volatile("" ::"v"(dw[0]), "v"(dw[R - 1]));
-#elif GX_TB_STORE_MODE == 4
-                // every store of the window gets its own data registers, all formed
-                // before the first store: no VALU write waits for a store to read
-                // the register it would overwrite (the compiler otherwise reuses one
-                // pair for all of them)
-                {
-                    uint2 sv[2][R / 4];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const uint32_t sel = h ? 0x07060302u : 0x05040100u;
-#pragma unroll
-                        for (int k = 0; k < R; k += 4) {
-                            sv[h][k / 4] = make_uint2(__builtin_amdgcn_perm(dw[k + 1], dw[k], sel),
-                                                      __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], sel));
-                            asm volatile("" : "+v"(sv[h][k / 4].x), "+v"(sv[h][k / 4].y));
-                        }
-                    }
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        if (valid[h] && w < W16[h]) {
-                            uint16_t *dst = reinterpret_cast<uint16_t *>(A.tb + (uint64_t)pr[h] * A.tb_pair_words) +
-                                            (uint64_t)w * (G * R) + lg * 4;
-#pragma unroll
-                            for (int k = 0; k < R; k += 4) *reinterpret_cast<uint2 *>(dst + k * G) = sv[h][k / 4];
-                        }
-                    }
-                }
+                    asm volatile("" ::"v"(dw[0]), "v"(dw[R - 1]));   // timing probe only: no direction stores
 #else
-                tb_store_window<G, R>(A, pr, valid, W16, w, lg, dw);   // layout: see tb_store_window
+                    tb_store_window<G, R>(A, pr, valid, W16, s >> 2, lg, dw);   // layout: see tb_store_window
 #endif
+                } else {
+                    half_step(flg, c, 0, HA, HB);
+                    half_step(flg, c + 1, 1, HB, HA);
+                }
             }
-#if GX_WF16_CAPTURE_TREE
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                fixv[h] = (int32_t)((capp[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
-#endif
+        };
+        // steps [0, G): lanes reset at column -1 (step lg - 1), captures of short pairs too;
+        // then steady steps, the capture window, steady steps
+        const uint32_t up = (cap_hi + STEP) & ~(STEP - 1);
+        run(std::integral_constant<int, 3>{}, min(nsteps, (uint32_t)G));
+        run(std::integral_constant<int, 0>{}, min(nsteps, cap_lo & ~(STEP - 1)));
+        run(std::integral_constant<int, 2>{}, min(nsteps, up));
+        run(std::integral_constant<int, 0>{}, nsteps);
+        if constexpr (GTB || GCP) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (fixable[h] && lg == kp_lane[h]) A.tbfix[pr[h]] = fixv[h];
-        } else {
-            for (uint32_t s = 0; s < nsteps; s += 2, c += 2) {
-                half_step(c, 0, HA, HB);
-                half_step(c + 1, 1, HB, HA);
-            }
-            if constexpr (GCP) {
-#if GX_WF16_CAPTURE_TREE
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    fixv[h] = (int32_t)((capp[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h]);
-#endif
-#pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    if (fixable[h] && lg == kp_lane[h]) A.tbfix[pr[h]] = fixv[h];
-            }
         }
-#if GX_WF16_CAPTURE_TREE
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-            score[h] = (int32_t)((capq[h] >> (16 * h)) & 0xFFFFu) - pb - D * (int32_t)(xl[h] + yl[h] - 2);
-#endif
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             if (valid[h] && lg == kq_lane[h]) A.score[pr[h]] = score[h];

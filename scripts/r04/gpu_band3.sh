@@ -19,3 +19,12 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --ti
 rc=$?; echo "packed rc=$rc $(tail -1 $O/packed.log)"; [ $rc -eq 0 ] || { tail -30 $O/packed.log; exit $rc; }
 timeout -k 10 300 python bench.py --workload semi --steps 10 --no-cpu --no-e2e --parity-pairs 200000 > $O/semi.json 2> $O/semi.err
 rc=$?; echo "semi rc=$rc"; python -c "import json; d=json.loads(open('$O/semi.json').read().strip().splitlines()[-1]); print('semi', d['value'], d['ms_per_step'], d['parity']['mismatches'], d['config']['plan'])"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "with_start or start" > $O/start.log 2>&1
+rc=$?; echo "start rc=$rc $(tail -1 $O/start.log)"; [ $rc -eq 0 ] || { tail -30 $O/start.log; exit $rc; }
+for v in "GASALX_START_STOP=1" "GASALX_START_STOP=0"; do
+  env $v timeout -k 10 300 python bench.py --workload sw_local_start --steps 10 --no-cpu --no-e2e --parity-pairs 200000 > "$O/st_$v.json" 2> "$O/st_$v.err"
+  rc=$?; [ $rc -eq 0 ] || { echo "bench $v rc=$rc"; tail -5 "$O/st_$v.err"; exit $rc; }
+  python -c "import json; d=json.loads(open('$O/st_$v.json').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['parity']['mismatches'], d['config']['plan'])"
+done
+timeout -k 10 300 python bench.py --workload sw_local --scores 2,4,6,1 --steps 10 --no-cpu --no-e2e --parity-pairs 200000 > $O/m2.json 2> $O/m2.err
+rc=$?; echo "m2 rc=$rc"; python -c "import json; d=json.loads(open('$O/m2.json').read().strip().splitlines()[-1]); print('match2', d['value'], d['ms_per_step'], d['parity']['mismatches'], d['config']['plan'])"

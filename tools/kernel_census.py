@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""VALU instruction mix of one kernel's steady loop, from the built library (gfx950 ISA).
+
+usage: kernel_census.py LIB.so KERNEL_SYMBOL [RATES.json]
+
+Extracts the gfx950 code object from the library's fat binary, disassembles the kernel,
+finds its loops (backward branches) and takes the one with the most VALU instructions as
+the steady state.  Each VALU instruction is priced by the issue-cost table measured with
+tools/ubench_issue.hip (cycles per wave64 instruction per SIMD at 8 waves per SIMD, bank-
+separated operands, s_memtime; profiles/r04_valu_issue_rates.json), by opcode, else by
+encoding class.  Prints JSON: counts per opcode, the VALU count and the average issue
+cycles per VALU instruction of the loop -- what tools/pmc_summary.py multiplies with the
+launch's SQ_INSTS_VALU to get the kernel's VALU issue cycles.
+"""
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def code_object(lib, tmp):
+    fat = os.path.join(tmp, "fat.bin")
+    subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, lib], check=True,
+                   capture_output=True)
+    co = os.path.join(tmp, "k.co")
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fat,
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True,
+                   capture_output=True)
+    return co
+
+
+def disasm(co, sym):
+    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", "--disassemble-symbols=" + sym, co],
+                         check=True, capture_output=True, text=True).stdout
+    ins = []   # (address, text, branch target offset or None); "<text>  // ADDR: RAW <sym+0xOFF>"
+    for line in out.splitlines():
+        m = re.match(r"^\s+(\S.*?)\s*//\s*([0-9A-Fa-f]+):", line)
+        if m:
+            t = re.search(r"<\S+\+0x([0-9a-f]+)>", line)
+            ins.append((int(m.group(2), 16), m.group(1).strip(), int(t.group(1), 16) if t else None))
+    return ins
+
+
+def rates_table(path):
+    d = json.load(open(path))
+    return {op: v.get("W8", v.get("W4")) for op, v in d["ops"].items()}
+
+
+def price(op, text, table):
+    base = re.sub(r"_e(32|64)$", "", op)
+    if "dpp" in text or "row_" in text or "wave_" in text:
+        return table.get("v_mov_b32_dpp", table.get("v_pk_add_u16", 4.0))
+    if base in table:
+        return table[base]
+    if base.startswith("v_pk_"):
+        return table.get("v_pk_add_u16", 4.0)
+    if base.startswith(("v_add3", "v_and_or", "v_or3", "v_bitop3", "v_lshl_add", "v_add_lshl", "v_lshl_or",
+                        "v_perm", "v_mad", "v_fma", "v_max3", "v_min3", "v_med3", "v_maximum3", "v_cndmask",
+                        "v_cmp", "v_mul_lo", "v_mul_hi")):
+        return table.get("v_add3_u32", 4.0) if not base.startswith("v_mul_lo") else 8.0
+    if base.startswith(("v_add_", "v_sub_", "v_subrev_", "v_and_", "v_or_", "v_xor_", "v_not_", "v_mov_",
+                        "v_mul_f32", "v_add_f32")):
+        return table.get("v_add_u32", 2.0)
+    return 4.0
+
+
+def census(lib, sym, rates):
+    table = rates_table(rates)
+    with tempfile.TemporaryDirectory() as tmp:
+        ins = disasm(code_object(lib, tmp), sym)
+    addr = {a: i for i, (a, _, _) in enumerate(ins)}
+    loops = []
+    for i, (a, t, off) in enumerate(ins):
+        if not t.startswith(("s_cbranch", "s_branch")) or off is None:
+            continue
+        tgt = ins[0][0] + off    # targets print relative to the symbol
+        if tgt in addr and addr[tgt] < i:
+            loops.append(ins[addr[tgt]:i + 1])
+    if not loops:
+        raise SystemExit("no loop found in " + sym)
+    # the steady column loop: the innermost loop carrying the DPP lane hand-offs (wavefront
+    # sweeps); kernels without them (band pass, thread-per-pair): the loop with the most packed
+    # or fp32 arithmetic, the shorter on ties
+    def dpp(seg):
+        return any(x.startswith("v_") and ("dpp" in x or "wave_shr" in x or "row_" in x) for _, x, _ in seg)
+
+    def arith(seg):
+        return sum(1 for _, x, _ in seg if x.startswith(("v_pk_", "v_fma", "v_fmac", "v_mul_f32", "v_perm")))
+    # densest in packed / fp32 arithmetic (the cell updates), among the DPP loops when there are any
+    with_dpp = [g for g in loops if dpp(g) and arith(g) > 0]
+    pool = with_dpp if with_dpp else [g for g in loops if arith(g) > 0] or loops
+    seg = max(pool, key=lambda g: (arith(g) / len(g), -len(g)))
+    best = (0, seg)
+    # static census: conditionally executed blocks (divergent captures, resets) are counted
+    # too, although the hardware skips them while no lane enters (s_cbranch_execz); the
+    # dynamic count is the PMC's SQ_INSTS_VALU
+    counts, cyc, nv = {}, 0.0, 0
+    for a, t, off in best[1]:
+        op = t.split()[0]
+        if not op.startswith("v_"):
+            continue
+        counts[op] = counts.get(op, 0) + 1
+        cyc += price(op, t, table)
+        nv += 1
+    return {"kernel": sym, "loop_valu": nv, "loop_issue_cycles": round(cyc, 2),
+            "cycles_per_valu": round(cyc / max(nv, 1), 4), "counts": dict(sorted(counts.items(), key=lambda x: -x[1])),
+            "rates": os.path.relpath(rates, ROOT)}
+
+
+if __name__ == "__main__":
+    rates = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "r04_valu_issue_rates.json")
+    print(json.dumps(census(sys.argv[1], sys.argv[2], rates), indent=1))
