@@ -45,7 +45,7 @@ void Workspace::release_all() {
     for (hipEvent_t *x : {&fork, &join, &dp_done})
         if (*x) { (void)hipEventDestroy(*x); *x = nullptr; }
     for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
-                      &rev_t, &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb}) b->release();
+                      &rev_t, &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb, &kseg}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -120,9 +120,9 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
 }
 
 static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false,
-                        bool lrs = false) {
+                        bool lrs = false, bool kseg = false) {
     if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
-                                                               : (ku16 || lrs) ? wf16_local_lookup(G, R, ku16, lrs)
+                                                               : (ku16 || lrs || kseg) ? wf16_local_lookup(G, R, ku16, lrs, kseg)
                                                                                : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
     return stop ? wf16_pick<WF16_SEMI_STOP>(G, R) : wf16_pick<WF_SEMI>(G, R);
@@ -358,12 +358,25 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
                 const int64_t span = (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8;
                 const bool frame = base + hmax + e * span + a + k + 64 <= 0x7BFF && base - 2 * e >= 0x400;
+                // past both, f16 keys by step segments of M = 2^m columns (WF16_LOCAL_SEG): (Hmax +
+                // 1) * M <= 0x7800 for any target length.  GASALX_KSEG=0: never, 2: before u16 keys
+                const char *ks = std::getenv("GASALX_KSEG");
+                const int kseg_mode = ks ? std::atoi(ks) : 1;
+                uint32_t mseg = 0;
+                while ((hmax + 1) * (int64_t)(2u << mseg) <= 0x7800 && mseg < 12) ++mseg;   // M = 2^mseg
+                const bool seg_ok = frame && kseg_mode > 0 && mseg >= 2 && y8 <= 0xFFFF;
                 if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) {
                     pl.kf16 = y8;
+                } else if (seg_ok && kseg_mode == 2) {
+                    pl.kf16 = y8;
+                    pl.kseg_shift = mseg;
                 } else if (frame && (hmax + 1) * (int64_t)y8 <= 0x10000 && y8 <= 0xFFFF &&
                            env_flag("GASALX_KU16", true)) {
                     pl.kf16 = y8;
                     pl.ku16 = true;
+                } else if (seg_ok) {
+                    pl.kf16 = y8;
+                    pl.kseg_shift = mseg;
                 }
                 if (pl.kf16) pl.key2 = false;
             }
@@ -391,7 +404,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             pl.name = std::string("wavefront16_") + an + (pl.tb ? (pl.tb_band ? "_tbband" : "_tb") : "") +
                       (pl.key2 ? "_k2" : "") +
                       (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && !pl.kf16 ? "_nodrift" : "") +
-                      (pl.ku16 ? "_u16" : "") + "_G" +
+                      (pl.ku16 ? "_u16" : "") + (pl.kseg_shift ? "_seg" + std::to_string(1u << pl.kseg_shift) : "") + "_G" +
                       std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
         else
             pl.name = std::string("wavefront_") + an + (pl.tb ? "_tb" : "") + (keys ? "_keys" : "") + "_G" +
@@ -458,7 +471,16 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         }
         WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
                               : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16,
-                                            A.lstop != nullptr && pl.kf16 != 0);
+                                            A.lstop != nullptr && pl.kf16 != 0 && !pl.kseg_shift, pl.kseg_shift != 0);
+        if (pl.kseg_shift) {
+            // the finished segments' keys per wave: saves at steps M, 2M, ... < nsteps <= C + G - 1
+            const uint32_t nsave = std::max<uint32_t>(1u, (pl.kf16 + (uint32_t)pl.G16 - 2u) >> pl.kseg_shift);
+            const uint64_t waves = (uint64_t)grid16 * kWavesPerBlock;
+            HIPCHK(ws.kseg.reserve(waves * nsave * (uint64_t)pl.R16 * 64 * 4 + 64));
+            P16.kseg = ws.kseg.as<uint32_t>();
+            P16.kseg_shift = pl.kseg_shift;
+            P16.kseg_n = nsave;
+        }
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
         if (pl.lds16_bytes > 64 * 1024)
             HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,

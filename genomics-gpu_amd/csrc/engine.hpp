@@ -36,6 +36,7 @@ struct Workspace {
     DevBuf sort_meta;               // length sort of the forward pass: perm, inverse, histogram
     DevBuf band_cp, band_stm, band_fl;   // GLOBAL+TB band recomputation: checkpoints, hand-offs, flags
     DevBuf band_fb;                 // its fallback: count, then the list of pairs, then the launch's flags
+    DevBuf kseg;                    // packed LOCAL keys by segments: the finished segments' keys per wave
     // traceback batches in chunks (align_device, GASALX_TB_CHUNKS): DPs on the
     // caller's stream, walks on walk_stream; one workspace per further chunk; all
     // created on first use
@@ -60,6 +61,7 @@ struct Plan {
     int32_t vmin = 0;       // packed GLOBAL/SEMI value-range bound
     uint32_t kf16 = 0;      // packed LOCAL: f16-pattern key columns (wavefront16.hpp step_local KU), 0 = 16-bit keys
     bool ku16 = false;      // packed LOCAL in the e-drift frame with u16 keys (WF16_LOCAL_U16)
+    uint32_t kseg_shift = 0; // packed LOCAL with f16 keys by step segments of 2^kseg_shift (WF16_LOCAL_SEG), 0 = off
     int G = 0, R = 0;
     uint32_t lds_stride = 0;
     size_t lds_bytes = 0;

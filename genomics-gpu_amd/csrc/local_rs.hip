@@ -1,6 +1,6 @@
 // local_rs.hip — instances of the packed LOCAL e-drift kernel (wavefront16.hpp) with u16 keys
 // (WF16_LOCAL_U16) and the WITH_START reverse pass's early stop (WF16_LOCAL_RS,
-// WF16_LOCAL_U16_RS), over the packed shapes of dispatch.hip kShapes16.  Compiled apart from
+// WF16_LOCAL_U16_RS) and with keys by step segments (WF16_LOCAL_SEG), over the packed shapes of dispatch.hip kShapes16.  Compiled apart from
 // dispatch.hip so the two build in parallel.
 #include "wavefront16.hpp"
 
@@ -16,7 +16,8 @@ static Wf16Fn pick(int G, int R) {
     return nullptr;
 }
 
-Wf16Fn wf16_local_lookup(int G, int R, bool u16, bool rs) {
+Wf16Fn wf16_local_lookup(int G, int R, bool u16, bool rs, bool seg) {
+    if (seg) return pick<WF16_LOCAL_SEG>(G, R);
     if (rs) return u16 ? pick<WF16_LOCAL_U16_RS>(G, R) : pick<WF16_LOCAL_RS>(G, R);
     return u16 ? pick<WF16_LOCAL_U16>(G, R) : pick<WF_LOCAL>(G, R);
 }

@@ -65,6 +65,10 @@ struct WfArgs {
     const uint32_t *n_dev;     // when set: the launch's pair count is *n_dev (<= n; traceback fallback list)
     const int32_t *lstop;      // LOCAL reverse pass of WITH_START (start.hpp): per pair the forward score; the
                                // e-drift sweep stops once every pair's first cell reaching it is settled
+    // LOCAL keys by step segments (wavefront16.hpp WF16_LOCAL_SEG): segment j = steps [j*2^kseg_shift,
+    // (j+1)*2^kseg_shift); the keys of every finished segment, [wave][segment < kseg_n][64 lanes][R]
+    uint32_t *kseg;
+    uint32_t kseg_shift, kseg_n;
 };
 
 constexpr int kWavesPerBlock = 4;

@@ -517,6 +517,12 @@ constexpr int WF16_SEMI_STOP = 9;
 constexpr int WF16_LOCAL_U16 = 10;    // LOCAL score + ends in the e-drift frame, u16 keys (step_local_dr U16)
 constexpr int WF16_LOCAL_RS = 11;     // LOCAL reverse pass of WITH_START (A.lstop early stop), f16 keys
 constexpr int WF16_LOCAL_U16_RS = 12; // the same with u16 keys (local_rs.hip instances)
+// LOCAL with f16-pattern keys by step segments: key = H*M + (M-1-t), t = the step within a
+// segment of M = 2^kseg_shift steps (lane lg: columns [jM - lg, (j+1)M - lg)), so the range
+// is (Hmax + 1) * M <= 0x7800 whatever the target length; at each segment's end (the same step
+// in every lane: no masked work) the keys go to A.kseg and restart; the final merge takes per
+// row the first segment holding its maximum (later columns win only when strictly higher)
+constexpr int WF16_LOCAL_SEG = 13;
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -548,12 +554,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
     constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16 || ALGO_ == WF16_LOCAL_U16_RS;
     constexpr bool LRS = ALGO_ == WF16_LOCAL_RS || ALGO_ == WF16_LOCAL_U16_RS;   // (the check costs VGPRs)
+    constexpr bool KSEG = ALGO_ == WF16_LOCAL_SEG;
     // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
     constexpr bool STOPK = ALGO_ == WF16_SEMI_STOP;
-    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16 || LRS) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16 || LRS || KSEG) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -719,7 +726,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         const bool any = valid[0] || valid[1];
         c = L;
         uint32_t fdummy = NN;
-        auto bstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R], const uint32_t t) {
+        auto bstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R], const uint32_t t) __attribute__((always_inline)) {
             const uint2 T = tcol[c + G];
             // H(-1, c - 1) at anti-diagonal c - 2 (the GLOBAL branch's dtop)
             const uint32_t dtop = (uint32_t)(pb + D * (c - 2) - (c <= 0 ? 0 : go + ge * c)) * 0x10001u;
@@ -752,6 +759,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         const uint32_t KMUL = A.one << 8;
         const uint32_t bshift = ((uint32_t)P.base << 8) & 0xFFFFu;
         uint32_t HA[R], HB[R], Ek[R], key[R], key2[K2 ? R : 1];
+        uint32_t jseg = 0;   // KSEG: segments saved to A.kseg (the live one is segment jseg)
 #pragma unroll
         for (int k = 0; k < R; ++k) { HA[k] = BB; HB[k] = BB; Ek[k] = BB; key[k] = 0; }
 #pragma unroll
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             uint32_t W16[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
-            auto qstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+            auto qstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) __attribute__((always_inline)) {
                 const uint2 T = tnext;
                 tnext = tcol[c + j + 1 + G];
                 step_local_tb<R>(T, c + j, top ? BB : prevRecvH, top ? BB : recvF, xs, Hin, Hout, Ek, key, dw, f, KK,
@@ -786,7 +794,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         } else {
             uint32_t s = 0;
             // two steps (ping-pong HA/HB) per iteration, up to step `end`
-            auto sweep = [&](auto kmc, const uint32_t end) {
+            auto sweep = [&](auto kmc, const uint32_t end) __attribute__((always_inline)) {
                 constexpr int KM = decltype(kmc)::value;
                 auto &k2 = *reinterpret_cast<uint32_t(*)[R]>(K2 ? key2 : key);   // unused unless K2
                 for (; s < end; s += 2, c += 2) {
@@ -819,15 +827,20 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // the garbage columns keep exactly (score 0, E at its floor), so they reach
                 // column -1 as the left boundary H = E = 0.  Top lane: diag H(-1, c-1) = 0,
                 // F(0, c) <= 0 (BB).
-                const uint32_t C = A.kf16, KMC = A.one * C;
+                const uint32_t C = A.kf16;
+                // key multiplier: the padded target length, or KSEG's segment length M
+                const uint32_t MK = KSEG ? (1u << A.kseg_shift) : C, KMC = A.one * MK;
                 const int32_t ge = A.e, pbv = P.base;
                 const uint32_t EXT2 = pk_bcast(2 * ge);
                 const uint32_t KXD = (uint32_t)((P.k - 2 * ge) * 0x10001),
                                OEXD = (uint32_t)((P.k - 2 * ge + A.o) * 0x10001);
                 constexpr uint32_t KOFS = KU16 ? 0u : 0x0400u;   // u16 keys need no f16 offset
-                auto inv = [&](int32_t cc, uint32_t add) {
-                    const uint32_t term = (cc >= 0 && (uint32_t)cc < C) ? C - 1u - (uint32_t)cc : 0u;
-                    return ((KOFS + term + add * C) & 0xFFFFu) * 0x10001u;
+                uint32_t segend = MK;                            // KSEG: the current segment's end step
+                auto inv = [&](int32_t cc, uint32_t add) __attribute__((always_inline)) {
+                    const uint32_t term = !(cc >= 0 && (uint32_t)cc < C) ? 0u
+                                          : KSEG ? segend - 1u - (uint32_t)(cc + (int32_t)lg)   // the step's rank
+                                                 : C - 1u - (uint32_t)cc;
+                    return ((KOFS + term + add * MK) & 0xFFFFu) * 0x10001u;
                 };
                 // Each lane keeps the frame shifted by its own constant, e(k + s) instead of
                 // e(r + c) (r = lg*R + k, c = s - lg): every floor FL[k] = B + e(k + s + 1) is
@@ -857,6 +870,14 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     for (int h = 0; h < 2; ++h) sstop[h] = valid[h] ? A.lstop[pr[h]] : 0;
                 }
                 for (; s < nsteps; s += 2, c += 2) {
+                    if (KSEG && s == segend && jseg < A.kseg_n) {   // wave-uniform: a segment ends
+                        // [wave][segment][lane][R]: one base address, immediate offsets
+                        uint32_t *dst = A.kseg + (((size_t)wv * A.kseg_n + jseg) * 64 + lane) * R;
+#pragma unroll
+                        for (int k = 0; k < R; ++k) { dst[k] = key[k]; key[k] = KOFS * 0x10001u; }
+                        ++jseg;
+                        segend += MK;
+                    }
                     uint2 T = tnext;
                     tnext = tcol[c + 1 + G];
                     const uint32_t dt0 = (uint32_t)(pbv + ge * (c - 2)) * 0x10001u;   // lane 0: H^(-1, c - 1)
@@ -903,7 +924,21 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 const uint32_t r = r0 + k;
                 const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
                 uint32_t H = kk >> 8, col = 255u - (kk & 0xFFu);
-                if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c) (u16 keys: no 0x0400)
+                if (KSEG) {
+                    // the first segment holding the row's maximum: the saved segments in order, then
+                    // the live one (keys 0x0400 + H*M + (M-1-t), t = the step within the segment)
+                    const uint32_t ms = A.kseg_shift;
+                    H = 0;
+                    col = 0;
+                    auto seg = [&](const uint32_t j, const uint32_t kv) __attribute__((always_inline)) {
+                        const uint32_t x = ((kv >> (16 * h)) & 0xFFFFu) - 0x0400u;
+                        const uint32_t Hj = x >> ms, t = x & ((1u << ms) - 1u);
+                        if (Hj > H) { H = Hj; col = ((j + 1) << ms) - 1u - t - lg; }
+                    };
+                    const uint32_t *src = A.kseg + ((size_t)wv * A.kseg_n * 64 + lane) * R + k;
+                    for (uint32_t j = 0; j < jseg; ++j) seg(j, src[(size_t)j * (64 * R)]);
+                    seg(jseg, key[k]);
+                } else if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c) (u16 keys: no 0x0400)
                     const uint32_t C = A.kf16, x = kk - (KU16 ? 0u : 0x0400u);
                     H = x / C;
                     col = C - 1u - (x - H * C);
@@ -1000,7 +1035,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         }
         // FLG bit 0: a lane may reach column -1 (its reset to the left boundary) in this
         // phase; bit 1: captures
-        auto half_step = [&](auto flg, const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+        auto half_step = [&](auto flg, const int32_t cc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) __attribute__((always_inline)) {
             constexpr int FLG = decltype(flg)::value;
             const uint2 T = tnext;
             tnext = tcol[cc + 1 + G];
@@ -1064,7 +1099,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
         constexpr uint32_t STEP = GTB ? 4 : 2;
         uint32_t s = 0;
-        auto run = [&](auto flg, const uint32_t end) {
+        auto run = [&](auto flg, const uint32_t end) __attribute__((always_inline)) {
             for (; s < end; s += STEP, c += STEP) {
                 if constexpr (GTB) {
                     half_step(flg, c, 0, HA, HB);
@@ -1084,11 +1119,17 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         };
         // steps [0, G): lanes reset at column -1 (step lg - 1), captures of short pairs too;
         // then steady steps, the capture window, steady steps
+        // (the full-matrix traceback kernel, now the band's fallback, keeps one loop: four copies
+        // of its flag sweep did not fit 256 VGPRs)
         const uint32_t up = (cap_hi + STEP) & ~(STEP - 1);
-        run(std::integral_constant<int, 3>{}, min(nsteps, (uint32_t)G));
-        run(std::integral_constant<int, 0>{}, min(nsteps, cap_lo & ~(STEP - 1)));
-        run(std::integral_constant<int, 2>{}, min(nsteps, up));
-        run(std::integral_constant<int, 0>{}, nsteps);
+        if constexpr (GTB) {
+            run(std::integral_constant<int, 3>{}, nsteps);
+        } else {
+            run(std::integral_constant<int, 3>{}, min(nsteps, (uint32_t)G));
+            run(std::integral_constant<int, 0>{}, min(nsteps, cap_lo & ~(STEP - 1)));
+            run(std::integral_constant<int, 2>{}, min(nsteps, up));
+            run(std::integral_constant<int, 0>{}, nsteps);
+        }
         if constexpr (GTB || GCP) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -1118,7 +1159,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // value the frame can hold and, undecayed, stays there)
         auto eleft = [=](int32_t r) -> uint32_t { return head_q ? (uint32_t)(pb + ge * (r - 1)) * 0x10001u : NN; };
         uint32_t HA[R], HB[R], Fk[R];
-        auto reset = [&](uint32_t (&H)[R]) {
+        auto reset = [&](uint32_t (&H)[R]) __attribute__((always_inline)) {
             // computed where used: hoisting 2R loop-invariant values out of the sweep would spill
             int32_t c0 = (int32_t)r0;
             asm volatile("" : "+v"(c0));
@@ -1155,7 +1196,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         const uint32_t hd_up = hm(head_t ? 0 : (r0 == 0 ? 0 : -(go + ge * (int32_t)r0)), -1, (int32_t)r0 - 1);
         uint32_t recvH = hd_up, prevRecvH = hd_up, recvE = NN, hl = 0, el = 0;
         uint2 tnext = tcol[c + G];
-        auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) {
+        auto half_step = [&](const int32_t cc, uint32_t (&Hin)[R], uint32_t (&Hout)[R]) __attribute__((always_inline)) {
             const uint2 T = tnext;
             tnext = tcol[cc + 1 + G];
             if (cc == -1) {
@@ -1247,6 +1288,6 @@ using Wf16Fn = void (*)(WfArgs);
 Wf16Fn wf16_tq_lookup(int R);
 // LOCAL e-drift instances with u16 keys and/or the reverse pass's early stop (local_rs.hip):
 // NULL for shapes outside kShapes16
-Wf16Fn wf16_local_lookup(int G, int R, bool u16, bool rs);
+Wf16Fn wf16_local_lookup(int G, int R, bool u16, bool rs, bool seg = false);
 
 }  // namespace gx

@@ -113,7 +113,8 @@ def test_local_drift_frame_length_edge(engine, scores):
     inside = edge_batch(_seed(scores, 0), 600, L)
     check(engine, inside, kw)
     past = plan(kw, L + 8, L + 8)
-    assert past.startswith(("wavefront16_local_u16_G", "wavefront16_local_nodrift_G", "wavefront_local")), past
+    assert past.startswith(("wavefront16_local_u16_G", "wavefront16_local_seg", "wavefront16_local_nodrift_G",
+                            "wavefront_local")), past
     check(engine, edge_batch(_seed(scores, 1), 600, L + 8), kw)
 
 
@@ -149,6 +150,36 @@ def test_local_u16_keys_config2_match2_and_long_targets(engine):
     b2 = G.Batch.from_pairs(qs, ts)
     assert plan(dict(algo=G.LOCAL), 150, 400).startswith("wavefront16_local_u16_G")
     check(engine, b2, dict(algo=G.LOCAL))
+
+
+@pytest.mark.parametrize("match", [1, 2, 3])
+def test_local_segment_keys_300(engine, match):
+    # 300 x 300 (config-3 data) past both single-key ranges: f16 keys by step segments
+    # (WF16_LOCAL_SEG), score + ends, short pairs and gaps beside them
+    kw = dict(algo=G.LOCAL, match=match)
+    name = plan(kw, 300, 300)
+    assert name.startswith("wavefront16_local_seg"), name
+    check(engine, G.Batch.synth(3, 6000, 0x5EED0300 + match), kw)
+    check(engine, edge_batch(_seed("seg", match), 1200, 300), kw)
+    check(engine, G.Batch.synth(3, 2000, 0x5EED0310 + match), dict(kw, start_pos=G.WITH_START))
+
+
+def test_local_segment_keys_match3_and_forced(engine, monkeypatch):
+    # config 2 at match 3 (outside u16), and GASALX_KSEG=2 (segments before u16 keys) at match 2,
+    # against the oracle; segment lengths from 8 (1 kb targets) up
+    b = G.Batch.synth(2, 20000, 0x5EED0003)
+    kw = dict(algo=G.LOCAL, match=3)
+    assert plan(kw, 150, 150).startswith("wavefront16_local_seg64_G")
+    check(engine, b, kw)
+    monkeypatch.setenv("GASALX_KSEG", "2")
+    assert plan(dict(algo=G.LOCAL, match=2), 150, 150).startswith("wavefront16_local_seg64_G")
+    check(engine, b, dict(algo=G.LOCAL, match=2))
+    monkeypatch.delenv("GASALX_KSEG")
+    rng = np.random.default_rng(78)
+    qs, ts = helpers.random_pairs(rng, 1500, 60, 150, 300, 500)
+    kw1 = dict(algo=G.LOCAL, match=2)
+    assert "_seg" in plan(kw1, 150, 500), plan(kw1, 150, 500)
+    check(engine, G.Batch.from_pairs(qs, ts), kw1)
 
 
 @pytest.mark.parametrize("L", [40, 150])

@@ -14,7 +14,7 @@
 #include <vector>
 
 constexpr int ITERS = 512;
-constexpr int PER_ITER = 32;   // 16 chains, the body twice
+constexpr int PER_ITER = 32;   // 16 chains, the body twice (packed fp32: 8 pair chains, the body four times)
 
 #define CLOB                                                                                               \
     "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", \
@@ -33,6 +33,22 @@ constexpr int PER_ITER = 32;   // 16 chains, the body twice
     S3(op, 37, 54, 55) S3(op, 38, 55, 56) S3(op, 39, 56, 57) S3(op, 40, 57, 58) S3(op, 41, 58, 59)         \
     S3(op, 42, 59, 60) S3(op, 43, 60, 61) S3(op, 44, 61, 62) S3(op, 45, 62, 63) S3(op, 46, 63, 48)         \
     S3(op, 47, 48, 49)
+// the same three-source ops with every operand in the destination's bank (bank conflicts)
+#define BODY3C(op)                                                                                          \
+    S3(op, 32, 48, 52) S3(op, 33, 49, 53) S3(op, 34, 50, 54) S3(op, 35, 51, 55) S3(op, 36, 56, 60)         \
+    S3(op, 37, 57, 61) S3(op, 38, 58, 62) S3(op, 39, 59, 63) S3(op, 40, 48, 52) S3(op, 41, 49, 53)         \
+    S3(op, 42, 50, 54) S3(op, 43, 51, 55) S3(op, 44, 56, 60) S3(op, 45, 57, 61) S3(op, 46, 58, 62)         \
+    S3(op, 47, 59, 63)
+// packed fp32 (64-bit register pairs): 8 chains, each counted once, the body four times
+#define P2(op, d, e, s, t) op " v[" #d ":" #e "], v[" #d ":" #e "], v[" #s ":" #t "]\n"
+#define P3(op, d, e, s, t, u, v) op " v[" #d ":" #e "], v[" #d ":" #e "], v[" #s ":" #t "], v[" #u ":" #v "]\n"
+#define BODYP2(op)                                                                                          \
+    P2(op, 32, 33, 50, 51) P2(op, 34, 35, 52, 53) P2(op, 36, 37, 54, 55) P2(op, 38, 39, 56, 57)              \
+    P2(op, 40, 41, 58, 59) P2(op, 42, 43, 60, 61) P2(op, 44, 45, 62, 63) P2(op, 46, 47, 48, 49)
+#define BODYP3(op)                                                                                          \
+    P3(op, 32, 33, 50, 51, 54, 55) P3(op, 34, 35, 52, 53, 58, 59) P3(op, 36, 37, 54, 55, 58, 59)             \
+    P3(op, 38, 39, 56, 57, 60, 61) P3(op, 40, 41, 58, 59, 62, 63) P3(op, 42, 43, 60, 61, 48, 49)             \
+    P3(op, 44, 45, 62, 63, 50, 51) P3(op, 46, 47, 48, 49, 52, 53)
 #define INIT                                                                                                \
     "v_mov_b32 v32, 0x3c003c00\nv_mov_b32 v33, 0x3c003c00\nv_mov_b32 v34, 0x3c003c00\nv_mov_b32 v35, 0x3c003c00\nv_mov_b32 v36, 0x3c003c00\n"          \
     "v_mov_b32 v37, 0x3c003c00\nv_mov_b32 v38, 0x3c003c00\nv_mov_b32 v39, 0x3c003c00\nv_mov_b32 v40, 0x3c003c00\nv_mov_b32 v41, 0x3c003c00\n"         \
@@ -73,16 +89,22 @@ KERNEL(k_pk_max_u16, BODY2("v_pk_max_u16"))
 KERNEL(k_pk_mad_u16, BODY3("v_pk_mad_u16"))
 KERNEL(k_pk_max_f16, BODY2("v_pk_max_f16"))
 KERNEL(k_pk_maximum3_f16, BODY3("v_pk_maximum3_f16"))
+KERNEL(k_fma_f32_conflict, BODY3C("v_fma_f32"))
+KERNEL(k_pk_fma_f32, BODYP3("v_pk_fma_f32") BODYP3("v_pk_fma_f32"))
+KERNEL(k_pk_mul_f32, BODYP2("v_pk_mul_f32") BODYP2("v_pk_mul_f32"))
+KERNEL(k_pk_add_f32, BODYP2("v_pk_add_f32") BODYP2("v_pk_add_f32"))
 
 typedef void (*Fn)(long long *);
 static const Fn ks[] = {k_add_u32,   k_sub_u32,    k_and_b32,   k_max_i32,    k_lshlrev_b32, k_add_f32,
                         k_mul_f32,   k_max_f32,    k_fma_f32,   k_fmac_f32,   k_add3_u32,    k_max3_i32,
                         k_perm_b32,  k_bitop3_b32, k_pk_add_u16, k_pk_sub_i16, k_pk_max_u16, k_pk_mad_u16,
-                        k_pk_max_f16, k_pk_maximum3_f16};
+                        k_pk_max_f16, k_pk_maximum3_f16, k_fma_f32_conflict, k_pk_fma_f32, k_pk_mul_f32,
+                        k_pk_add_f32};
 static const char *names[] = {"v_add_u32",    "v_sub_u32",    "v_and_b32",    "v_max_i32",     "v_lshlrev_b32",
                               "v_add_f32",    "v_mul_f32",    "v_max_f32",    "v_fma_f32",     "v_fmac_f32",
                               "v_add3_u32",   "v_max3_i32",   "v_perm_b32",   "v_and_or_b32",  "v_pk_add_u16",
-                              "v_pk_sub_i16", "v_pk_max_u16", "v_pk_mad_u16", "v_pk_max_f16",  "v_pk_maximum3_f16"};
+                              "v_pk_sub_i16", "v_pk_max_u16", "v_pk_mad_u16", "v_pk_max_f16",  "v_pk_maximum3_f16",
+                              "v_fma_f32_bank_conflict", "v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32"};
 
 int main() {
     int cus = 0;
