@@ -300,6 +300,7 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         shape.max_q = mq;
         shape.max_t = mt;
         shape.sort = gx::uneven_lengths(*params, hb->q_lens + i0, hb->t_lens + i0, m);
+        shape.one_t8 = gx::one_pad8(hb->t_lens + i0, m);
         shape.tb_split = false;   // the two slots' streams already overlap one chunk's walk with the next DP
         if ((rc = gx::align_device(s.ws, *params, db, dout, s.st, shape))) {
             for (HostSlot &x : eng->slot) (void)hipStreamSynchronize(x.st);
@@ -382,6 +383,7 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     shape.max_q = db.max_q_len;
     shape.max_t = db.max_t_len;
     shape.sort = gx::uneven_lengths(*params, hb->q_lens, hb->t_lens, n);
+    shape.one_t8 = gx::one_pad8(hb->t_lens, n);
     rc = gx::align_device(eng->ws, *params, db, dout, st, shape);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
 #define BACK(h, d, cnt)                                                                             \

@@ -515,7 +515,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
 // synchronisation of the stream), flags per slot; then the int32 kernel over the slots
 // the packed launches declined.
 static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p, const WfArgs &base,
-                          hipStream_t st) {
+                          hipStream_t st, bool one_class) {
     WfArgs A = base;
     const uint32_t n = A.n;
     A.a = p.match; A.b = p.mismatch; A.o = p.gap_open; A.e = p.gap_extend;
@@ -529,12 +529,17 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     const size_t sh = (size_t)(t8w + 1) * 4;
     HIPCHK(ws.sort_meta.reserve((size_t)n * 4 + 2 * sh + 64));
     uint32_t *perm = ws.sort_meta.as<uint32_t>(), *hist = perm + n, *cursor = hist + t8w + 1;
-    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, hist);
-    HIPCHK(hipGetLastError());
-    std::vector<uint32_t> h(t8w + 1);
-    HIPCHK(hipMemcpyAsync(h.data(), hist, sh, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint32_t> h(t8w + 1, 0u);
+    if (one_class) {
+        h[0] = n;   // every pair in the largest class (host-side lengths, BatchShape::one_t8): no read-back
+    } else {
+        // the class sizes, read back: one synchronisation of the stream (gasalx.h, max_t_len)
+        HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+        rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, hist);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(h.data(), hist, sh, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
     int classes = 0;
     for (uint32_t b = 0; b <= t8w; b++) classes += h[b] != 0;
     A.perm = nullptr;
@@ -733,10 +738,10 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     // buffer (get_tb.h:94) but the packed kernels' walk reads query codes from it:
     // give it a copy, taken before any walk runs
     const uint8_t *walk_qseq = nullptr;
+    const bool cigar_on_query = out.cigar && (const uint8_t *)out.cigar < b.q_batch + b.q_bytes &&
+                                b.q_batch < (const uint8_t *)out.cigar + (cigar_cap ? cigar_cap : b.q_bytes);
     if (runs_tb && out.cigar && out.n_cigar_ops && pl.kind == PLAN_WAVEFRONT && pl.packed16 && !pl.need_pack) {
-        const uint8_t *c0 = out.cigar, *q0 = b.q_batch;
-        const uint64_t cap = cigar_cap ? cigar_cap : b.q_bytes;
-        if (c0 < q0 + b.q_bytes && q0 < c0 + cap) {
+        if (cigar_on_query) {
             HIPCHK(ws.packed_q.reserve(b.q_bytes));
             HIPCHK(hipMemcpyAsync(ws.packed_q.p, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
             walk_qseq = ws.packed_q.as<uint8_t>();
@@ -747,8 +752,11 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     // walk (tb_kernel) bound by the latency of its dependent loads.  Chunk k's DP runs
     // on the caller's stream, its walk on a second stream after an event, beside the
     // following DPs.  Every chunk has its own workspace (direction data, flags, ends).
+    // A chunk's walk writes CIGARs over the query bytes of its pairs while the next chunk's DP
+    // runs: when the CIGAR buffer is the query batch, every chunk's DP reads the copy taken
+    // above (pairs may share query bytes, one-to-many), and without a copy there is no split
     const bool can_split = runs_tb && out.cigar && out.n_cigar_ops && shape.tb_split && pl.kind == PLAN_WAVEFRONT &&
-                           !pl.need_pack;
+                           !pl.need_pack && (!cigar_on_query || walk_qseq);
     // Tail split (GASALX_TB_TAIL=1, A/B): the pairs that fill whole rounds of the packed
     // DP kernel's wave slots, then the rest.  Chunk 0's walk runs on the second stream
     // beside chunk 1's DP (the DP's last, partly filled round), chunk 1's walk follows
@@ -771,6 +779,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
             for (uint32_t c = 0; c < 2 && rc == GASALX_OK; c++) {
                 const uint32_t i0 = c ? n0 : 0, m = c ? n - n0 : n0;
                 gasalx_batch cb = b;
+                if (walk_qseq) cb.q_batch = walk_qseq;
                 cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
                 if (cb.q_ops) cb.q_ops += i0;
                 if (cb.t_ops) cb.t_ops += i0;
@@ -814,6 +823,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         for (uint32_t c = 0, i0 = 0; i0 < n && rc == GASALX_OK; c++, i0 += per) {
             const uint32_t m = std::min(per, n - i0);
             gasalx_batch cb = b;
+            if (walk_qseq) cb.q_batch = walk_qseq;
             cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
             if (cb.q_ops) cb.q_ops += i0;
             if (cb.t_ops) cb.t_ops += i0;
@@ -960,7 +970,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             A.band_wd = pl.band_wd;
             fb_count = ws.band_fb.as<uint32_t>();
         }
-        int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st) : launch_wavefront(ws, pl, p, A, st);
+        int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st, shape.one_t8) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start && dp) {
             if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {

@@ -80,6 +80,8 @@ struct BatchShape {
     bool sort = false;   // lengths are uneven: run the wavefront kernels over pairs sorted by step-axis length
     uint32_t n = 0;      // pairs in the launch (0 = unknown: shapes for large batches)
     bool tb_split = true; // traceback: chunks on two streams so a chunk's walk overlaps the next DP
+    bool one_t8 = false;  // host-side lengths: every padded target length is the same (SEMI TAIL=QUERY/BOTH
+                          // then launches its one class without reading the class histogram back)
 };
 
 Plan make_plan(const gasalx_params &p, const BatchShape &shape, bool has_ops);
@@ -97,6 +99,15 @@ inline bool uneven_lengths(const gasalx_params &p, const uint32_t *q_lens, const
         hi = w > hi ? w : hi;
     }
     return hi >= lo + 2;
+}
+
+// Host-side check for BatchShape::one_t8: one padded target length in the batch.
+inline bool one_pad8(const uint32_t *t_lens, uint32_t n) {
+    if (!t_lens || n == 0) return false;
+    const uint32_t w = (t_lens[0] + 7) >> 3;
+    for (uint32_t i = 1; i < n; i++)
+        if (((t_lens[i] + 7) >> 3) != w) return false;
+    return true;
 }
 
 // Launch the full path for a device-resident batch on `stream`.

@@ -78,7 +78,12 @@ typedef struct gasalx_batch {
     const uint8_t *t_ops;
     const uint32_t *seed_scores;  /* KSW h0 per pair, or NULL */
     uint32_t max_q_len;           /* upper bound of q_lens (0 = unknown: the engine reads   */
-    uint32_t max_t_len;           /* the lengths back, which synchronises the stream)       */
+    uint32_t max_t_len;           /* the lengths back, which synchronises the stream).      */
+                                  /* SEMI_GLOBAL with TAIL = QUERY/BOTH, score only, reads  */
+                                  /* back the histogram of padded target lengths (one sync */
+                                  /* of the stream) even when both are given; the host     */
+                                  /* entry points skip it when every target has the same   */
+                                  /* padded length                                         */
 } gasalx_batch;
 
 /* Output arrays (n_alns entries; cigar has q_bytes entries).  NULL = not wanted.

@@ -149,6 +149,27 @@ def test_multi_allgather_rccl():
     assert _gather_case(devs, rccl=True) is True
 
 
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="needs two distinct GPUs (ADVICE r03: the distinct-device "
+                                                "shard and peer-copy paths)")
+def test_multi_distinct_devices_align_and_gather():
+    # distinct devices: one engine per GPU (cross-device event waits, hipMemcpyPeerAsync of the
+    # results) and the allgather over a communicator of distinct devices, against the oracle
+    devs = list(range(min(_device_count(), 4)))
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET)
+    b = G.Batch.synth(4, 40_000, 0x5EED0004)
+    m = G.Multi(devs)
+    g = m.align_host(b, G.make_params(**kw), fields=["score", "q_end", "t_end"])
+    m.close()
+    _check_all(g, O.align(b, O.make_params(**kw)), ("score", "q_end", "t_end"))
+    assert _gather_case(devs, rccl=False) is False      # peer copies between distinct devices
+    assert _gather_case(devs, rccl=True) is True
+
+
 @pytest.mark.parametrize("workload,pairs,checked", [("semi", 200_000, 200_000), ("nw_tb", 20_000, 40_000)])
 def test_bench_two_ranks_gloo_one_gpu(workload, pairs, checked):
     # the exact N = 2 bench path on one device: torch.distributed.run spawns 2 ranks, each
