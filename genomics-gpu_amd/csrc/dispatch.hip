@@ -365,12 +365,14 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 uint32_t mseg = 0;
                 while ((hmax + 1) * (int64_t)(2u << mseg) <= 0x7800 && mseg < 12) ++mseg;   // M = 2^mseg
                 const bool seg_ok = frame && kseg_mode > 0 && mseg >= 2 && y8 <= 0xFFFF;
-                if (frame && (hmax + 1) * (int64_t)y8 <= 0x7800) {
+                // key range: steps C + G (GX_LOCAL_UKEY, wavefront16.hpp) or columns C
+                const int64_t kc = (int64_t)y8 + (GX_LOCAL_UKEY ? pl.G16 : 0);
+                if (frame && (hmax + 1) * kc <= 0x7800) {
                     pl.kf16 = y8;
                 } else if (seg_ok && kseg_mode == 2) {
                     pl.kf16 = y8;
                     pl.kseg_shift = mseg;
-                } else if (frame && (hmax + 1) * (int64_t)y8 <= 0x10000 && y8 <= 0xFFFF &&
+                } else if (frame && (hmax + 1) * kc <= 0x10000 && y8 <= 0xFFFF &&
                            env_flag("GASALX_KU16", true)) {
                     pl.kf16 = y8;
                     pl.ku16 = true;

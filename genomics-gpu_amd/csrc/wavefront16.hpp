@@ -59,6 +59,11 @@ typedef unsigned short pk_u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_mad_u16(uint32_t a, uint32_t b, uint32_t c) {
     return GX_AS(uint32_t, GX_AS(pk_u2, a) * GX_AS(pk_u2, b) + GX_AS(pk_u2, c));
 }
+// c's low half added to both halves (a splat the compiler issues as op_sel_hi on an SGPR)
+__device__ __forceinline__ uint32_t pk_mad_u16_lo(uint32_t a, uint32_t b, uint32_t c) {
+    const pk_u2 cc = {(uint16_t)c, (uint16_t)c};
+    return GX_AS(uint32_t, GX_AS(pk_u2, a) * GX_AS(pk_u2, b) + cc);
+}
 __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
     return GX_AS(uint32_t, __builtin_elementwise_max(GX_AS(pk_u2, a), GX_AS(pk_u2, b)));
 }
@@ -94,6 +99,9 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 #endif
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
+#endif
+#ifndef GX_LOCAL_UKEY
+#define GX_LOCAL_UKEY 1   // LOCAL e-drift keys with wave-uniform addends (0: per-lane subtracts, A/B)
 #endif
 #ifndef GX_WF16_K2_WAVES
 #define GX_WF16_K2_WAVES 2    // LOCAL over 257..512 target columns (a 3-wave build spills)
@@ -225,8 +233,13 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                                               uint32_t (&Ek)[R], uint32_t (&key)[R], uint32_t (&FL)[R],
                                               uint32_t &f_out, const uint32_t KX, const uint32_t OEX,
                                               const uint32_t EXT, const uint32_t KMUL, const uint32_t invp,
-                                              const uint32_t invn, const uint32_t EXT2) {
+                                              const uint32_t invn, const uint32_t EXT2, const uint32_t MK16 = 0) {
     uint32_t diag = diag_top, f = f_top;
+#if GX_LOCAL_UKEY
+    // row 0's addends (invp / invn: the candidates' bases), then one scalar subtract per row
+    const uint32_t g20 = (FL[0] - EXT2) & 0xFFFFu, EM = (EXT2 >> 1 & 0xFFFFu) * MK16;   // e * M
+    uint32_t a1 = invp - g20 * MK16, a2 = invn - g20 * MK16;
+#endif
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
@@ -236,6 +249,17 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
         Ek[k] = pk_max3(toe, Ek[k], FL[k]);
         if (KEYS) {
+#if GX_LOCAL_UKEY
+            // key = (H^ - g2) * M + base = H^ * M + (base - g2 * M) (mod 2^16): the addend is the
+            // same in every lane (FL and the step's bases are wave-uniform), so it is scalar work
+            // and a cell pair's keys cost two mads and one max (the subtracts are gone)
+            if (U16)
+                key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2)));
+            else
+                key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
+            a1 -= EM;   // row k + 1: FL one e higher
+            a2 -= EM;
+#else
             // 32-bit subtracts, borrow-free: Hin >= FL - 2e and H >= FL - e
             const uint32_t g2 = pk_subnb(FL[k], EXT2);
             const uint32_t d1 = pk_subnb(Hin[k], g2), d2 = pk_subnb(H, g2);
@@ -243,6 +267,7 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                 key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn)));
             else
                 key[k] = pk_max3(key[k], pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn));
+#endif
         }
         FL[k] = pk_addnc(FL[k], EXT);
         f = pk_max_u16(toe, f);
@@ -828,20 +853,37 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // column -1 as the left boundary H = E = 0.  Top lane: diag H(-1, c-1) = 0,
                 // F(0, c) <= 0 (BB).
                 const uint32_t C = A.kf16;
-                // key multiplier: the padded target length, or KSEG's segment length M
-                const uint32_t MK = KSEG ? (1u << A.kseg_shift) : C, KMC = A.one * MK;
+                // key multiplier: KSEG's segment length M, else the step range C + G (GX_LOCAL_UKEY:
+                // keys rank steps, not columns, so that their addend is wave-uniform) or C
+                const uint32_t CP = GX_LOCAL_UKEY ? C + G : C;
+                const uint32_t MK = KSEG ? (1u << A.kseg_shift) : CP, KMC = A.one * MK;
                 const int32_t ge = A.e, pbv = P.base;
                 const uint32_t EXT2 = pk_bcast(2 * ge);
                 const uint32_t KXD = (uint32_t)((P.k - 2 * ge) * 0x10001),
                                OEXD = (uint32_t)((P.k - 2 * ge + A.o) * 0x10001);
                 constexpr uint32_t KOFS = KU16 ? 0u : 0x0400u;   // u16 keys need no f16 offset
                 uint32_t segend = MK;                            // KSEG: the current segment's end step
+#if GX_LOCAL_UKEY
+                uint32_t KMV = KMC;
+                asm volatile("" : "+v"(KMV));   // the multiplier in a VGPR: the mads' scalar operand is the addend
+#else
+                const uint32_t KMV = KMC;
+#endif
+#if GX_LOCAL_UKEY
+                // the key base of the candidate at step ss: KOFS + (end - 1 - ss) + add * M, end = the
+                // segment's end step (KSEG) or C + G; the garbage columns left of the matrix hold H = 0
+                // and those right of it less than the maximum, so no column test is needed
+                auto inv = [&](uint32_t ss, uint32_t add) __attribute__((always_inline)) {
+                    return (KOFS + ((KSEG ? segend : CP) - 1u - ss) + add * MK) & 0xFFFFu;
+                };
+#else
                 auto inv = [&](int32_t cc, uint32_t add) __attribute__((always_inline)) {
                     const uint32_t term = !(cc >= 0 && (uint32_t)cc < C) ? 0u
                                           : KSEG ? segend - 1u - (uint32_t)(cc + (int32_t)lg)   // the step's rank
                                                  : C - 1u - (uint32_t)cc;
                     return ((KOFS + term + add * MK) & 0xFFFFu) * 0x10001u;
                 };
+#endif
                 // Each lane keeps the frame shifted by its own constant, e(k + s) instead of
                 // e(r + c) (r = lg*R + k, c = s - lg): every floor FL[k] = B + e(k + s + 1) is
                 // then the same in all lanes (scalar registers, s_add per step) and the
@@ -889,8 +931,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     T = tnext;
                     tnext = tcol[c + 2 + G];
                     const uint32_t dt1 = (uint32_t)(pbv + ge * (c - 1)) * 0x10001u;
+#if GX_LOCAL_UKEY
+                    step_local_dr<R, true, KU16>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
+                                           KXD, OEXD, EXT, KMV, inv(s, 0), inv(s + 1, (uint32_t)(-ge)), EXT2, MK);
+#else
                     step_local_dr<R, true, KU16>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
                                            KXD, OEXD, EXT, KMC, inv(c, 0), inv(c + 1, (uint32_t)(-ge)), EXT2);
+#endif
                     prevRecvH = recvH;
                     recvH = pk_subnb((uint32_t)shr_lane((int32_t)HA[R - 1]), ADJ);
                     recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
@@ -904,7 +951,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                             bool hit[2];
 #pragma unroll
                             for (int h = 0; h < 2; ++h) {
-                                const uint32_t thr = KOFS + (uint32_t)sstop[h] * C + (C - 1u - (uint32_t)m);
+                                // (the key of column m: step m + lg, GX_LOCAL_UKEY; else column m)
+                                const uint32_t thr = KOFS + (uint32_t)sstop[h] * MK +
+                                                     (GX_LOCAL_UKEY ? CP - 1u - (uint32_t)m - lg : C - 1u - (uint32_t)m);
                                 hit[h] = !valid[h] || sstop[h] <= 0 || ((mx >> (16 * h)) & 0xFFFFu) >= thr;
                             }
                             if (groups_all<G>(__ballot(hit[0])) && groups_all<G>(__ballot(hit[1]))) break;
@@ -939,9 +988,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     for (uint32_t j = 0; j < jseg; ++j) seg(j, src[(size_t)j * (64 * R)]);
                     seg(jseg, key[k]);
                 } else if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c) (u16 keys: no 0x0400)
-                    const uint32_t C = A.kf16, x = kk - (KU16 ? 0u : 0x0400u);
+                    const uint32_t C = A.kf16 + (GX_LOCAL_UKEY ? G : 0), x = kk - (KU16 ? 0u : 0x0400u);
                     H = x / C;
-                    col = C - 1u - (x - H * C);
+                    col = C - 1u - (x - H * C) - (GX_LOCAL_UKEY ? lg : 0u);   // (the step's rank, GX_LOCAL_UKEY)
                 }
                 if constexpr (K2) {   // columns 256..511: later, so they win only when strictly higher
                     const uint32_t k2v = (key2[k] >> (16 * h)) & 0xFFFFu;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU instruction mix of one kernel's steady loop, from the built library (gfx950 ISA).
 
-usage: kernel_census.py LIB.so KERNEL_SYMBOL [RATES.json]
+usage: kernel_census.py LIB.so|OBJ.co KERNEL_SYMBOL [RATES.json]
 
 Extracts the gfx950 code object from the library's fat binary, disassembles the kernel,
 finds its loops (backward branches) and takes the one with the most VALU instructions as
@@ -47,6 +47,8 @@ def disasm(co, sym):
 
 
 def rates_table(path):
+    if not os.path.exists(path):
+        return {}
     d = json.load(open(path))
     return {op: v.get("W8", v.get("W4")) for op, v in d["ops"].items()}
 
@@ -72,7 +74,7 @@ def price(op, text, table):
 def census(lib, sym, rates):
     table = rates_table(rates)
     with tempfile.TemporaryDirectory() as tmp:
-        ins = disasm(code_object(lib, tmp), sym)
+        ins = disasm(lib if lib.endswith(".co") else code_object(lib, tmp), sym)   # .co: a gfx950 code object
     addr = {a: i for i, (a, _, _) in enumerate(ins)}
     loops = []
     for i, (a, t, off) in enumerate(ins):
@@ -99,15 +101,16 @@ def census(lib, sym, rates):
     # static census: conditionally executed blocks (divergent captures, resets) are counted
     # too, although the hardware skips them while no lane enters (s_cbranch_execz); the
     # dynamic count is the PMC's SQ_INSTS_VALU
-    counts, cyc, nv = {}, 0.0, 0
+    counts, cyc, nv, ns = {}, 0.0, 0, 0
     for a, t, off in best[1]:
         op = t.split()[0]
+        ns += op.startswith("s_")
         if not op.startswith("v_"):
             continue
         counts[op] = counts.get(op, 0) + 1
         cyc += price(op, t, table)
         nv += 1
-    return {"kernel": sym, "loop_valu": nv, "loop_issue_cycles": round(cyc, 2),
+    return {"kernel": sym, "loop_valu": nv, "loop_salu": ns, "loop_issue_cycles": round(cyc, 2),
             "cycles_per_valu": round(cyc / max(nv, 1), 4), "counts": dict(sorted(counts.items(), key=lambda x: -x[1])),
             "rates": os.path.relpath(rates, ROOT)}
 
