@@ -120,8 +120,9 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
 }
 
 static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false,
-                        bool lrs = false, bool kseg = false) {
-    if (algo == WF_LOCAL) return tb ? wf16_pick_local_tb(G, R) : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
+                        bool lrs = false, bool kseg = false, bool tbd = false) {
+    if (algo == WF_LOCAL) return tb ? (tbd ? wf16_pick_r4<WF16_LOCAL_TBD>(G, R) : wf16_pick_local_tb(G, R))
+                                    : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
                                                                : (ku16 || lrs || kseg) ? wf16_local_lookup(G, R, ku16, lrs, kseg)
                                                                                : wf16_pick<WF_LOCAL>(G, R);
     if (algo == WF_GLOBAL) return tb ? wf16_pick_tb(G, R) : wf16_pick<WF_GLOBAL>(G, R);
@@ -163,9 +164,9 @@ static bool packed16_ok(const gasalx_params &p, int wf_algo, uint32_t mq, uint32
         *vmin = 0;
         // 16-bit keys H*256 + col: 256 columns each, a second key set up to 512 (not with traceback)
         if (local_key16_ok(p, mq, mt)) return true;
-        // the e-drift score kernels key on H*C + col (f16 patterns or u16): make_plan checks
-        // their frame and key range for the chosen shape
-        return p.start_pos != 2 && env_flag("GASALX_KF16", true);
+        // the e-drift kernels key on H*C + col (f16 patterns or u16; traceback: f16): make_plan
+        // checks their frame and key range for the chosen shape
+        return env_flag("GASALX_KF16", true);
     }
     int64_t k, top, drift = 0;
     if (wf_algo == WF_SEMI) {
@@ -352,7 +353,10 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             // the window and the top lane's first diagonal B - 2e above 0x0400.  GASALX_KF16=0
             // keeps the round-2 kernel, GASALX_KU16=0 the int32 kernel where only u16 keys fit
             // (A/B runs)
-            if (wf_algo == WF_LOCAL && !pl.tb && env_flag("GASALX_KF16", true)) {
+            // LOCAL + traceback takes the e-drift kernel with f16 keys (WF16_LOCAL_TBD) when they fit;
+            // GASALX_LTBD=0 keeps the round-2 traceback kernel (A/B)
+            if (wf_algo == WF_LOCAL && env_flag("GASALX_KF16", true) &&
+                (!pl.tb || (GX_LOCAL_UKEY && env_flag("GASALX_LTBD", true)))) {
                 const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
                 const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
                 const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
@@ -369,6 +373,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 const int64_t kc = (int64_t)y8 + (GX_LOCAL_UKEY ? pl.G16 : 0);
                 if (frame && (hmax + 1) * kc <= 0x7800) {
                     pl.kf16 = y8;
+                } else if (pl.tb) {
+                    // (the traceback kernel has f16 keys only)
                 } else if (seg_ok && kseg_mode == 2) {
                     pl.kf16 = y8;
                     pl.kseg_shift = mseg;
@@ -406,6 +412,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             pl.name = std::string("wavefront16_") + an + (pl.tb ? (pl.tb_band ? "_tbband" : "_tb") : "") +
                       (pl.key2 ? "_k2" : "") +
                       (wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && !pl.kf16 ? "_nodrift" : "") +
+                      (wf_algo == WF_LOCAL && pl.tb && pl.kf16 ? "_dr" : "") +
                       (pl.ku16 ? "_u16" : "") + (pl.kseg_shift ? "_seg" + std::to_string(1u << pl.kseg_shift) : "") + "_G" +
                       std::to_string(pl.G16) + "R" + std::to_string(pl.R16);
         else
@@ -473,7 +480,8 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         }
         WfFn f16 = pl.tb_band ? wf16_pick_r4<WF16_GLOBAL_CP>(pl.G16, pl.R16)
                               : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16,
-                                            A.lstop != nullptr && pl.kf16 != 0 && !pl.kseg_shift, pl.kseg_shift != 0);
+                                            A.lstop != nullptr && pl.kf16 != 0 && !pl.kseg_shift, pl.kseg_shift != 0,
+                                            pl.tb && pl.kf16 != 0);
         if (pl.kseg_shift) {
             // the finished segments' keys per wave: saves at steps M, 2M, ... < nsteps <= C + G - 1
             const uint32_t nsave = std::max<uint32_t>(1u, (pl.kf16 + (uint32_t)pl.G16 - 2u) >> pl.kseg_shift);

@@ -341,6 +341,62 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
     return __builtin_amdgcn_bitop3_b32(a, m, b, 0xEA);
 }
 
+// ---------------------------------------------------------------------------
+// LOCAL + traceback in the e-drift frame (WF16_LOCAL_TBD): step_local_dr's cell (no E or F
+// extension subtract, E floored at FL, F unfloored as the reference's) plus the four
+// "differs" flags of step_local_tb in the same skewed layout: u = [H != tmp], w = [H != F],
+// x = [E' != E - e], y = [F' != F - e] -- in the frame E - e and F - e are the stored E^ and F^.
+// With F unfloored, w and y are the reference's own tests on every cell; x differs from the
+// reference only where E is floored (E <= 0), never on a gap run the walk follows (it stops
+// before H = 0, get_tb.h:100-103).  Keys: the wave-uniform addends of step_local_dr
+// (GX_LOCAL_UKEY), two columns per v_pk_maximum3 on the KEYS steps.  15.5 instructions per cell
+// pair instead of step_local_tb's 19.
+// ---------------------------------------------------------------------------
+template <int R, bool KEYS>
+__device__ __forceinline__ void step_local_tb_dr(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
+                                                 const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
+                                                 uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
+                                                 uint32_t &FL0, uint32_t (&dw)[R], uint32_t &f_out,
+                                                 const uint32_t KX, const uint32_t OEX, const uint32_t EXT,
+                                                 const uint32_t KMUL, const uint32_t invp, const uint32_t invn,
+                                                 const uint32_t EXT2, const uint32_t MK16, const int j) {
+    const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
+    uint32_t diag = diag_top, f = f_top;
+    // the rows' floors FL0 + k e are formed per row from row 0's (scalar adds): an array of R
+    // floors in scalar registers overflowed them at this kernel's two waves (readlane spills)
+    const uint32_t g20 = (FL0 - EXT2) & 0xFFFFu, EM = ((EXT2 >> 1) & 0xFFFFu) * MK16;
+    uint32_t a1 = invp - g20 * MK16, a2 = invn - g20 * MK16, flk = FL0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
+        const uint32_t t1 = pk_addnc(diag, v);
+        const uint32_t tmp = pk_subnb(t1, KX);
+        const uint32_t toe = pk_subnb(t1, OEX);
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        const uint32_t En = pk_max3(toe, Ek[k], flk);
+        const uint32_t Fn = pk_max_u16(toe, f);
+        const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, Ek[k]), fy = tb_flag(toe, f);
+        const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
+        const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
+        dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
+        if (KEYS) {
+            key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
+            a1 -= EM;
+            a2 -= EM;
+        }
+        flk = pk_addnc(flk, EXT);   // row k + 1: one e higher
+        Ek[k] = En;
+        f = Fn;
+        diag = Hin[k];
+        Hout[k] = H;
+        // row by row, the scalar chains too (the scheduler otherwise spills, VGPRs and SGPRs)
+        if (KEYS) asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(a1), "+s"(a2), "+s"(flk));
+        else asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(flk));
+    }
+    FL0 = pk_addnc(FL0, EXT);   // the next step
+    f_out = f;
+}
+
 template <int R, bool SYNC = false>
 __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
@@ -548,6 +604,10 @@ constexpr int WF16_LOCAL_U16_RS = 12; // the same with u16 keys (local_rs.hip in
 // in every lane: no masked work) the keys go to A.kseg and restart; the final merge takes per
 // row the first segment holding its maximum (later columns win only when strictly higher)
 constexpr int WF16_LOCAL_SEG = 13;
+constexpr int WF16_LOCAL_TBD = 14;    // LOCAL + traceback in the e-drift frame (step_local_tb_dr)
+#ifndef GX_WF16_LTBD_WAVES
+#define GX_WF16_LTBD_WAVES 2
+#endif
 #ifndef GX_WF16_TQ_WAVES
 #define GX_WF16_TQ_WAVES 3
 #endif
@@ -565,6 +625,7 @@ constexpr int WF16_LOCAL_SEG = 13;
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                    : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
+                                   : ALGO_ == WF16_LOCAL_TBD ? GX_WF16_LTBD_WAVES
                                    : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES
                                    : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? GX_WF16_TQ_BIG_WAVES : GX_WF16_TQ_WAVES)
                                    : ALGO_ == WF16_GLOBAL_CP ? GX_WF16_CP_WAVES
@@ -580,12 +641,13 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16 || ALGO_ == WF16_LOCAL_U16_RS;
     constexpr bool LRS = ALGO_ == WF16_LOCAL_RS || ALGO_ == WF16_LOCAL_U16_RS;   // (the check costs VGPRs)
     constexpr bool KSEG = ALGO_ == WF16_LOCAL_SEG;
+    constexpr bool LTBD = ALGO_ == WF16_LOCAL_TBD;
     // TQ: one launch per class of equal padded target length G*R (dispatch.hip), so the
     // last padded column is always register R - 1 of lane G - 1
     constexpr bool TQ = ALGO_ == WF16_SEMI_TQ;
     static_assert(!TQ || G == 8, "TAIL=QUERY/BOTH instances are G = 8");
     constexpr bool STOPK = ALGO_ == WF16_SEMI_STOP;
-    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16 || LRS || KSEG) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
+    constexpr int ALGO = GT ? WF_GLOBAL : (LTB || K2 || KU16 || LRS || KSEG || LTBD) ? WF_LOCAL : (TQ || STOPK) ? WF_SEMI : ALGO_;
     constexpr int S = 64 / G;            // lane groups per wave
     constexpr bool TR = ALGO == WF_SEMI; // transposed: X = target, Y = query
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -911,7 +973,41 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                     for (int h = 0; h < 2; ++h) sstop[h] = valid[h] ? A.lstop[pr[h]] : 0;
                 }
-                for (; s < nsteps; s += 2, c += 2) {
+#if GX_LOCAL_UKEY
+                if constexpr (LTBD) {
+                    // four steps per window of direction flags (tb_store_window, the LOCAL_TB layout);
+                    // the keys of two columns on the second step of each pair
+                    static_assert(R % 4 == 0, "LOCAL+TB packed shapes need R % 4 == 0");
+                    uint32_t dw[R];
+#pragma unroll
+                    for (int k = 0; k < R; ++k) dw[k] = 0;
+                    uint32_t W16[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) W16[h] = (ypad[h] + G + 2) >> 2;
+                    uint32_t FL0 = FL[0];
+                    auto tstep = [&](auto keysc, const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R])
+                        __attribute__((always_inline)) {
+                        constexpr bool KEYS = decltype(keysc)::value;
+                        const uint2 T = tnext;
+                        tnext = tcol[c + j + 1 + G];
+                        const uint32_t dt = (uint32_t)(pbv + ge * (c + j - 2)) * 0x10001u;   // lane 0: H^(-1, c + j - 1)
+                        step_local_tb_dr<R, KEYS>(T, top ? dt : prevRecvH, top ? BB : recvF, xs, Hin, Hout, Ek, key, FL0,
+                                                  dw, f, KXD, OEXD, EXT, KMV, KEYS ? inv(s + j - 1, 0) : 0u,
+                                                  KEYS ? inv(s + j, (uint32_t)(-ge)) : 0u, EXT2, MK, j);
+                        prevRecvH = recvH;
+                        recvH = pk_subnb((uint32_t)shr_lane((int32_t)Hout[R - 1]), ADJ);
+                        recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
+                    };
+                    for (; s < nsteps; s += 4, c += 4) {
+                        tstep(std::false_type{}, 0, HA, HB);
+                        tstep(std::true_type{}, 1, HB, HA);
+                        tstep(std::false_type{}, 2, HA, HB);
+                        tstep(std::true_type{}, 3, HB, HA);
+                        tb_store_window<G, R>(A, pr, valid, W16, s >> 2, lg, dw);   // layout: see tb_store_window
+                    }
+                }
+#endif
+                for (; !LTBD && s < nsteps; s += 2, c += 2) {
                     if (KSEG && s == segend && jseg < A.kseg_n) {   // wave-uniform: a segment ends
                         // [wave][segment][lane][R]: one base address, immediate offsets
                         uint32_t *dst = A.kseg + (((size_t)wv * A.kseg_n + jseg) * 64 + lane) * R;

@@ -30,6 +30,8 @@ step localtests 600 $PYT tests/test_gpu_parity.py -k "local"
 step tbtests 600 $PYT tests/test_gpu_parity.py -k "global or kat or config3 or traceback"
 run nw_tb "X=1" nw_tb --steps 10 --parity-pairs 100000
 run nw_tb_full "GASALX_TB_BAND=0" nw_tb --steps 10 --parity-pairs 100000
+run sw_local_tb "X=1" sw_local_tb --steps 6 --parity-pairs 100000
+run sw_local_tb_old "GASALX_LTBD=0" sw_local_tb --steps 6 --parity-pairs 100000
 run sw_local_300 "X=1" sw_local_300 --steps 5 --parity-pairs 50000
 run semi "X=1" semi --steps 5 --parity-pairs 200000
 run pairhmm "X=1" pairhmm --steps 10 --parity-pairs 100000

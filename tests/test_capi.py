@@ -67,7 +67,7 @@ def test_plan_selection_cpu_only():
     # past the u16 range: f16 keys by 64-step segments (WF16_LOCAL_SEG); GASALX_KSEG=0: the int32 kernel
     assert G.describe_plan(G.make_params(algo=G.LOCAL, match=3), 150, 150) == "wavefront16_local_seg64_G8R19"
     assert G.describe_plan(G.make_params(algo=G.LOCAL), 300, 300) == "wavefront16_local_seg64_G16R20"
-    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB), 150, 150) == "wavefront16_local_tb_G8R20"
+    assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB), 150, 150) == "wavefront16_local_tb_dr_G8R20"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_TB, match=2), 150, 150) == \
         "wavefront_local_tb_keys_G8R20"
     assert G.describe_plan(G.make_params(algo=G.LOCAL, start_pos=G.WITH_START), 150, 150) == \
