@@ -172,17 +172,24 @@ def test_local_with_start_packed_and_ops(engine):
 
 @pytest.mark.parametrize("alphabet,scores", [(b"ACGT", (1, 4, 6, 1)), (b"ACGTN", (2, 3, 5, 2)),
                                              (b"ACGTRY", (1, 4, 6, 1))])
-def test_local_long_targets_two_keys(engine, alphabet, scores):
-    # packed LOCAL over 257..512 target columns keeps a second key set per row
+def test_local_long_targets_two_keys(engine, monkeypatch, alphabet, scores):
+    # packed LOCAL over 257..512 target columns: the round-2 kernel's second key set per row
+    # (GASALX_KF16=0), and the e-drift kernels the planner takes by default (u16 keys or
+    # step segments), on the same pairs
     a, bb, o, e = scores
     kw = dict(algo=G.LOCAL, match=a, mismatch=bb, gap_open=o, gap_extend=e)
-    assert G.describe_plan(G.make_params(**kw), 120, 512) == "wavefront16_local_k2_G8R16"
+    default = G.describe_plan(G.make_params(**kw), 120, 512)
+    assert default.startswith(("wavefront16_local_u16_G8R16", "wavefront16_local_seg")), default
     rng = np.random.default_rng(zlib.crc32(repr((alphabet, scores)).encode()) & 0xFFFF)
     qs, ts = helpers.random_pairs(rng, 1500, 1, 120, 200, 512, alphabet=alphabet, related=0.5)
     # ties across the 256-column boundary: a repeated block on both sides of it
     rep = helpers.random_seq(rng, 40)
     qs += [rep] * 20
     ts += [helpers.random_seq(rng, 230 + i) + rep + helpers.random_seq(rng, 10) + rep for i in range(20)]
+    check(engine, G.Batch.from_pairs(qs, ts), **kw)
+    check(engine, G.Batch.from_pairs(qs[:600], ts[:600]), start_pos=G.WITH_START, **kw)
+    monkeypatch.setenv("GASALX_KF16", "0")
+    assert G.describe_plan(G.make_params(**kw), 120, 512) == "wavefront16_local_k2_G8R16"
     check(engine, G.Batch.from_pairs(qs, ts), **kw)
     check(engine, G.Batch.from_pairs(qs[:600], ts[:600]), start_pos=G.WITH_START, **kw)
 

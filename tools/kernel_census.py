@@ -50,7 +50,7 @@ def rates_table(path):
     if not os.path.exists(path):
         return {}
     d = json.load(open(path))
-    return {op: v.get("W8", v.get("W4")) for op, v in d["ops"].items()}
+    return {op: v.get("W2") for op, v in d["ops"].items()}   # the SIMD rate (see the file's "reading")
 
 
 def price(op, text, table):
