@@ -1002,7 +1002,9 @@ def test_local_global_every_packed_shape(engine, monkeypatch, algo, g, r):
     for a, bb, o, e in [(1, 4, 6, 1), (1, 3, 5, 2), (1, 2, 2, 1)]:
         kw = dict(algo=algo, match=a, mismatch=bb, gap_open=o, gap_extend=e)
         plan = G.describe_plan(G.make_params(**kw), ql, 240)
-        assert plan == f"wavefront16_{'local' if algo == G.LOCAL else 'global'}_G{g}R{r}", plan
+        # (LOCAL: f16 or u16 keys in the e-drift frame, whichever the key range allows)
+        assert plan.startswith(f"wavefront16_{'local' if algo == G.LOCAL else 'global'}_") and \
+            plan.endswith(f"_G{g}R{r}") and "start" not in plan, plan
         check(engine, b, **kw)
 
 
