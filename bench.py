@@ -67,6 +67,9 @@ WORKLOADS = {
     "sw_local_300": dict(kind=3, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL), bytes=632, ops=12,
                          label="config-3 data (300 x 300, target = mutated query) through SW local score+ends, "
                                "1M pairs per GPU (VERDICT r03 item 5: past the single-key window)"),
+    "nw_score": dict(kind=3, pairs=100_000, scaling="weak", params=dict(algo=G.GLOBAL), bytes=624, ops=16,
+                     label="config-3 data, NW global score only (no traceback), 100K pairs x 300bp per GPU: the "
+                           "sweep the band traceback's first pass is built on"),
     "nw_tb": dict(kind=3, pairs=100_000, scaling="weak", params=dict(algo=G.GLOBAL, start_pos=G.WITH_TB), bytes=650,
                   ops=16, streams=2, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
     "semi": dict(kind=4, pairs=10_000_000, scaling="strong",
@@ -108,6 +111,7 @@ METRICS = {
     "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
     "ksw": "GCUPS of GASAL2 KSW extension (config-2 data, 1M x 150bp) on MI355X",
     "sw_local_300": "GCUPS of batched 300bp affine-gap SW local (config-3 data) on MI355X",
+    "nw_score": "GCUPS of batched 300bp affine-gap NW global score (config-3 data) on MI355X",
 }
 SEEDS = {1: 0x5EED0001, 2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005, 6: 0x5EED0006}
 

@@ -50,6 +50,9 @@ __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' |
 #ifndef GX_HMM_PKFMA
 #define GX_HMM_PKFMA 0   // 1: the I and MM FMAs of a cell as one v_pk_fma_f32 (A/B: 4,574 vs 5,242 GCUPS, r03_pairhmm_ab.md)
 #endif
+#ifndef GX_HMM_PREFETCH
+#define GX_HMM_PREFETCH 1   // table rows one column ahead in a second register set (0: loaded in place)
+#endif
 #ifndef GX_HMM_WAVES
 #define GX_HMM_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
@@ -238,7 +241,15 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
             for (int m = 32; m >= 1; m >>= 1) hmin = min(hmin, (uint32_t)__shfl_xor(hmin, m));
             const uint32_t s1 = min((uint32_t)G - 1, nsteps), s2 = max(s1, hmin);
             for (uint32_t s = 0; s < s1; ++s) checked_step(s);
-            if constexpr (TABP) {
+            if constexpr (TABP && !GX_HMM_PREFETCH) {
+                // one register set: each column's table rows loaded where the column starts
+                // (8 VGPRs fewer; the other waves of the SIMD cover the LDS latency)
+                for (uint32_t s = s1; s < hmin; ++s) {
+                    float aa[RR];
+                    tload(hap[s - lg], aa);
+                    steady(aa);
+                }
+            } else if constexpr (TABP) {
                 // table rows one step ahead, two register sets in turn (hap reads past a
                 // pair's columns stay inside the slot + table region and are not used)
                 float aaA[RR], aaB[RR];

@@ -589,6 +589,9 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 //    path leaves it to a WF16_GLOBAL_TB launch over the full matrix (dispatch.hip).
 // Per cell pair the sweep issues 7 instructions instead of step_global_tb's 15; the band is
 // R x wd of every lane's G*R x (ypad) cells (config 3, w = 12: 44 of 304 columns).
+// entries per lane of the band hand-off stream: wd + 1 used, rounded up to blocks of 4, plus the
+// two blocks the band pass prefetches past its last one
+__host__ __device__ constexpr uint32_t band_stream_words(uint32_t wd) { return ((wd + 1 + 3) & ~3u) + 8; }
 constexpr int WF16_GLOBAL_CP = 7;
 constexpr int WF16_GLOBAL_BAND = 8;
 // SEMI TAIL=TARGET reverse pass of WITH_START (start.hpp, A.stop): the forward instances keep
@@ -619,7 +622,7 @@ constexpr int WF16_LOCAL_TBD = 14;    // LOCAL + traceback in the e-drift frame 
 #define GX_WF16_CP_WAVES 3    // GLOBAL score sweep with band checkpoints
 #endif
 #ifndef GX_WF16_BAND_WAVES
-#define GX_WF16_BAND_WAVES 4  // band recomputation with flags (122 VGPRs)
+#define GX_WF16_BAND_WAVES 3  // band recomputation with flags (136 VGPRs with the stream blocks in flight)
 #endif
 
 template <int ALGO_, int G, int R>
@@ -803,31 +806,36 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             HB[k] = HA[k];
             dw[k] = 0;
         }
-        // the upper lane's stream, two entries ahead (lane 0 reads a neighbour's and ignores it)
-        const uint2 *sp = A.stm + (size_t)wv * (WD + 1) * 64 + (lane ? lane - 1 : 0);
-        uint2 e0 = sp[0], e1 = sp[64], e2 = sp[128];
+        // the upper lane's stream (lane 0 reads a neighbour's and ignores it), [wave][lane][SW]:
+        // blocks of 4 entries as two 16-byte loads, the block two ahead in flight (the loads
+        // of one entry two steps ahead stalled the pass on their latency)
+        const uint32_t SW = band_stream_words(WD);
+        const uint4 *sp = reinterpret_cast<const uint4 *>(A.stm + ((size_t)wv * 64 + (lane ? lane - 1 : 0)) * SW);
+        uint4 B0a = sp[0], B0b = sp[1], B1a = sp[2], B1b = sp[3];
         // a window from column 0 starts at the left boundary: H(r0 - 1, -1) (Q2; lane 0 of the
         // sweep never runs column -1, so lane 1's entry 0 is not stored)
-        if (L == 0) e0.x = (uint32_t)(pb + D * ((int32_t)r0 - 2) - (r0 <= 1 ? 0 : go + ge * ((int32_t)r0 - 1))) * 0x10001u;
+        if (L == 0) B0a.x = (uint32_t)(pb + D * ((int32_t)r0 - 2) - (r0 <= 1 ? 0 : go + ge * ((int32_t)r0 - 1))) * 0x10001u;
         uint4 *bf = A.bflags + ((size_t)wv * 64 + lane) * (WD / 4) * (R / 4);
         const bool any = valid[0] || valid[1];
         c = L;
         uint32_t fdummy = NN;
-        auto bstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R], const uint32_t t) __attribute__((always_inline)) {
+        // entry t: (H(r0 - 1, c - 1), F(r0, c)) for c = L + t - 1 ... step j of a block takes the
+        // diagonal from entry j and F from entry j + 1
+        auto bstep = [&](const int j, uint32_t (&Hin)[R], uint32_t (&Hout)[R], const uint32_t hd, const uint32_t fu)
+            __attribute__((always_inline)) {
             const uint2 T = tcol[c + G];
             // H(-1, c - 1) at anti-diagonal c - 2 (the GLOBAL branch's dtop)
             const uint32_t dtop = (uint32_t)(pb + D * (c - 2) - (c <= 0 ? 0 : go + ge * c)) * 0x10001u;
-            step_global_tb<R, true>(T, top ? dtop : e0.x, top ? NN : e1.y, xs, Hin, Hout, Ek, dw, fdummy, KX, OEX, NN, j);
-            e0 = e1;
-            e1 = e2;
-            e2 = sp[(size_t)min(t + 3, WD) * 64];
+            step_global_tb<R, true>(T, top ? dtop : hd, top ? NN : fu, xs, Hin, Hout, Ek, dw, fdummy, KX, OEX, NN, j);
             ++c;
         };
         for (uint32_t t = 0; t < WD; t += 4) {
-            bstep(0, HA, HB, t);
-            bstep(1, HB, HA, t + 1);
-            bstep(2, HA, HB, t + 2);
-            bstep(3, HB, HA, t + 3);
+            const uint4 B2a = sp[t / 2 + 4], B2b = sp[t / 2 + 5];   // entries t + 8 .. t + 11
+            bstep(0, HA, HB, B0a.x, B0a.w);
+            bstep(1, HB, HA, B0a.z, B0b.y);
+            bstep(2, HA, HB, B0b.x, B0b.w);
+            bstep(3, HB, HA, B0b.z, B1a.y);
+            B0a = B1a; B0b = B1b; B1a = B2a; B1b = B2b;
             if (any) {
                 uint4 *dst = bf + (t / 4) * (R / 4);
 #pragma unroll
@@ -1152,7 +1160,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         const bool cp_on = GCP && (valid[0] || valid[1]);
         const bool st_on = cp_on && lg + 1 < G;
         uint32_t *cpw = GCP ? A.cp + ((size_t)wv * 64 + lane) * (2 * R) : nullptr;   // [wave][lane][2R]
-        uint2 *stw = GCP ? A.stm + (size_t)wv * (A.band_wd + 1) * 64 + lane : nullptr;
+        uint2 *stw = GCP ? A.stm + ((size_t)wv * 64 + lane) * band_stream_words(A.band_wd) : nullptr;   // [wave][lane][SW]
         uint2 tnext = tcol[c + G];
         // Capture window: the steps at which some lane of the wave holds a cell to capture --
         // row xl - 1 at column yl - 1 (the score, global.h:98-103,299) and, for traceback, row
@@ -1229,7 +1237,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     }
                 }
                 const uint32_t t = (uint32_t)(cc - cs_dn);
-                if (st_on && t <= A.band_wd) stw[(size_t)t * 64] = make_uint2(Hout[R - 1], f);
+                if (st_on && t <= A.band_wd) stw[t] = make_uint2(Hout[R - 1], f);
             }
             prevRecvH = recvH;
             recvH = (uint32_t)shr_lane((int32_t)Hout[R - 1]);
