@@ -497,7 +497,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
                                        (int)pl.lds16_bytes));
         hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
         HIPCHK(hipGetLastError());
-        if (pl.tb_band) {   // the band pass over the blocks the sweep aligned (same grid and slots)
+        if (pl.tb_band && !GX_TB_FUSED) {   // the band pass over the blocks the sweep aligned (same grid and slots)
             WfFn fb = wf16_pick_r4<WF16_GLOBAL_BAND>(pl.G16, pl.R16);
             if (!fb) { set_error("no packed band instance"); return GASALX_EUNSUPPORTED; }
             if (pl.lds16_bytes > 64 * 1024)

@@ -54,7 +54,7 @@ __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' |
 #define GX_HMM_PREFETCH 1   // table rows one column ahead in a second register set (0: loaded in place)
 #endif
 #ifndef GX_HMM_WAVES
-#define GX_HMM_WAVES 3   // waves per SIMD the register allocator must allow
+#define GX_HMM_WAVES 4   // waves per SIMD the register allocator must allow (4: 128 VGPRs + 16 B of scratch, 5,551 against 5,309 GCUPS at 3, profiles/r04/pairhmm_4w.json)
 #endif
 template <int G, int RR, bool QUALS = false, bool ABS = false>
 __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {

@@ -618,6 +618,9 @@ constexpr int WF16_LOCAL_TBD = 14;    // LOCAL + traceback in the e-drift frame 
 #define GX_WF16_TQ_BIG_WAVES 3   // R > 20 (A/B knob): 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
 #endif
 
+#ifndef GX_TB_FUSED
+#define GX_TB_FUSED 1   // GLOBAL+TB: the band pass inside the checkpoint sweep's kernel (0: its own launch)
+#endif
 #ifndef GX_WF16_CP_WAVES
 #define GX_WF16_CP_WAVES 3    // GLOBAL score sweep with band checkpoints
 #endif
@@ -781,7 +784,12 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     const bool top = lg == 0;
     int32_t c = -(int32_t)lg;                            // step-axis position of this lane
 
-    if constexpr (GBD) {
+    // Band recomputation (WF16_GLOBAL_BAND, or the sweep kernel itself once its sweep is done,
+    // GX_TB_FUSED): lane lg's rows r0..r0+R-1 over the columns [L, L + wd), L = max(r0 - w, 0),
+    // from the state the WF16_GLOBAL_CP sweep stored (same frame, same tables, so
+    // step_global_tb sees the inputs the full traceback sweep would).
+    auto band_pass = [&]() __attribute__((always_inline)) {
+      if constexpr (GBD || GCP) {
         // Band recomputation (WF16_GLOBAL_BAND): lane lg's rows r0..r0+R-1 over the columns
         // [L, L + wd), L = max(r0 - w, 0), from the state WF16_GLOBAL_CP stored (same frame,
         // same tables, so step_global_tb sees the inputs the full traceback sweep would).
@@ -846,6 +854,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                             __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x07060302u));
             }
         }
+      }
+    };
+    if constexpr (GBD) {
+        band_pass();
         return;
     }
 
@@ -1291,6 +1303,12 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             if (valid[h] && lg == kq_lane[h]) A.score[pr[h]] = score[h];
+        if constexpr (GCP && GX_TB_FUSED) {
+            // the band pass right behind the sweep, in the same wave: no second prologue, and the
+            // checkpoints and hand-offs just written (this wave's own stores) are read from L2
+            __threadfence_block();
+            band_pass();
+        }
     } else {
         // SEMI, transposed: c is the query row of this step, registers are the
         // target columns lg*R + k.  Boundaries (semiglobal_kernel_template.h):
