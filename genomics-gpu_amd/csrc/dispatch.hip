@@ -645,6 +645,7 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     R.nval = (uint32_t)(p.n_code & 0xF);
     R.perm = perm;
     const uint64_t items = (uint64_t)n * (R.q8w + R.t8w);
+    rev_len_kernel<<<grid_for(n, 256), 256, 0, st>>>(R);
     rev_prep_kernel<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(R);
     HIPCHK(hipGetLastError());
     gasalx_params pr = p;

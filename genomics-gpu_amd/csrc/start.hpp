@@ -196,33 +196,40 @@ __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const ui
     }
 }
 
-// one thread per (slot, 8-base word of the two reversed sequences of the slot's pair)
+// one thread per slot: the reversed lengths (LOCAL: the end words, less the trailing N pads, a
+// loop of dependent byte loads done once per pair) and the slot's offsets
+__global__ __launch_bounds__(256) void rev_len_kernel(RevArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t k = A.perm[i];
+    const uint32_t ql = A.qlen[k];
+    uint32_t L = ql;
+    if (A.mode == REV_LOCAL) {
+        const uint32_t off = A.qoff[k];
+        L = 8 * start_regs(ql, A.qend[k]);
+        while (L > ql && seq_byte(A.q, off, L - 1, A.packed) % 16u == A.nval) --L;
+    }
+    A.rqoff[i] = i * A.q8w * 8;
+    A.rqlen[i] = L;
+    A.rtoff[i] = i * A.t8w * 8;
+    A.rtlen[i] = rev_tlen(A.mode, A.tlen, A.tend, k);
+    if (A.stop) A.stop[i] = A.score[k];
+}
+
+// one thread per (slot, 8-base word of the two reversed sequences of the slot's pair), the
+// lengths from rev_len_kernel
 __global__ __launch_bounds__(256) void rev_prep_kernel(RevArgs A) {
     const uint32_t per = A.q8w + A.t8w;
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (uint64_t)A.n * per) return;
     const uint32_t i = (uint32_t)(gid / per), w = (uint32_t)(gid - (uint64_t)i * per);
     const uint32_t k = A.perm[i];
-    if (w < A.q8w) {
-        const uint32_t ql = A.qlen[k], off = A.qoff[k];
-        uint32_t L = ql;
-        if (A.mode == REV_LOCAL) {
-            L = 8 * start_regs(ql, A.qend[k]);
-            while (L > ql && seq_byte(A.q, off, L - 1, A.packed) % 16u == A.nval) --L;
-        }
-        *reinterpret_cast<uint2 *>(A.rq + (uint64_t)i * A.q8w * 8 + 8u * w) = rev_first(A.q, off, L, w, A.packed, A.fill);
-        if (w == 0) {
-            A.rqoff[i] = i * A.q8w * 8;
-            A.rqlen[i] = L;
-            if (A.stop) A.stop[i] = A.score[k];
-        }
-    } else {
-        const uint32_t ww = w - A.q8w;
-        const uint32_t L = rev_tlen(A.mode, A.tlen, A.tend, k);
-        *reinterpret_cast<uint2 *>(A.rt + (uint64_t)i * A.t8w * 8 + 8u * ww) =
-            rev_first(A.t, A.toff[k], L, ww, A.packed, A.fill);
-        if (ww == 0) { A.rtoff[i] = i * A.t8w * 8; A.rtlen[i] = L; }
-    }
+    if (w < A.q8w)
+        *reinterpret_cast<uint2 *>(A.rq + (uint64_t)i * A.q8w * 8 + 8u * w) =
+            rev_first(A.q, A.qoff[k], A.rqlen[i], w, A.packed, A.fill);
+    else
+        *reinterpret_cast<uint2 *>(A.rt + (uint64_t)i * A.t8w * 8 + 8u * (w - A.q8w)) =
+            rev_first(A.t, A.toff[k], A.rtlen[i], w - A.q8w, A.packed, A.fill);
 }
 
 // one thread per slot i (pair perm[i])
