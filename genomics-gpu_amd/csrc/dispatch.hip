@@ -972,7 +972,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             const uint64_t waves = (uint64_t)grid_for(n, ppb16) * kWavesPerBlock;
             HIPCHK(ws.band_cp.reserve(waves * 2 * pl.R16 * 64 * 4 + 64));
             HIPCHK(ws.band_stm.reserve(waves * 64 * band_stream_words(pl.band_wd) * 8 + 64));
-            HIPCHK(ws.band_fl.reserve(waves * 64 * band_diags(pl.band_wd, pl.R16) * (pl.R16 / 4) * 16 + 64));
+            HIPCHK(ws.band_fl.reserve(waves * 64 * (pl.band_wd / 4) * (pl.R16 / 4) * 16 + 64));
             HIPCHK(ws.band_fb.reserve((size_t)n * 4 + grid_for(n, ppb16) + 256));
             A.cp = ws.band_cp.as<uint32_t>();
             A.stm = ws.band_stm.as<uint2>();

@@ -585,7 +585,7 @@ struct TbArgs {
     const uint32_t *toff;
     int32_t seq_packed, nval, has_npen, npen;
     // band recomputation (wavefront16.hpp WF16_GLOBAL_BAND): packed pairs read the flags of
-    // their lane's band window ([wave][64][diagonal][R/4] uint4, two pairs per entry); a path that
+    // their lane's band window ([wave][64][wd/4][R/4] uint4, two pairs per entry); a path that
     // leaves the band appends its pair to fb_list and stops (its bytes so far are a prefix of
     // the CIGAR the full-matrix walk writes later)
     const uint4 *band;
@@ -626,11 +626,9 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     const bool pk = A.pk_flags && A.pk_flags[slot / A.pk_ppb];
     const bool bnd = pk && A.band;
     // band layout: this pair's half of its lane group's entries in wave slot / pk_ppw
-    // (diagonal-major: [lane][d = window - row group + R/4 - 1][row group], wavefront16.hpp)
-    const uint32_t bR4 = A.pk_R / 4, bND = A.band_wd / 4 + bR4 - 1;
     const uint2 *bnd2 = bnd ? reinterpret_cast<const uint2 *>(A.band) +
                                   ((uint64_t)(slot / A.pk_ppw) * 64 + ((slot % A.pk_ppw) >> 1) * A.pk_G) *
-                                      (bND * bR4) * 2 + (slot & 1u)
+                                      ((A.band_wd / 4) * (A.pk_R / 4)) * 2 + (slot & 1u)
                             : nullptr;
     bool out_of_band = false;
     // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
@@ -670,7 +668,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 const int32_t L = max((int32_t)(lane * A.pk_R) - (int32_t)A.band_w, 0);
                 const uint32_t t = (uint32_t)((int32_t)col - L);
                 if (t >= A.band_wd) { out_of_band = true; break; }
-                const int64_t key = (((int64_t)lane * bND + (t >> 2) - (k >> 2) + bR4 - 1) * bR4 + (k >> 2)) * 2;
+                const int64_t key = (((int64_t)lane * (A.band_wd / 4) + (t >> 2)) * (A.pk_R / 4) + (k >> 2)) * 2;
                 if (key != chunk_key) {
                     const uint2 c2 = bnd2[key];
                     chunk = make_uint4(c2.x, c2.y, 0u, 0u);

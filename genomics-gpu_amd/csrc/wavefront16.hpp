@@ -592,8 +592,6 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 // entries per lane of the band hand-off stream: wd + 1 used, rounded up to blocks of 4, plus the
 // two blocks the band pass prefetches past its last one
 __host__ __device__ constexpr uint32_t band_stream_words(uint32_t wd) { return ((wd + 1 + 3) & ~3u) + 8; }
-// diagonals of 4 x 4 flag chunks per lane in the band's diagonal-major layout
-__host__ __device__ constexpr uint32_t band_diags(uint32_t wd, uint32_t r) { return wd / 4 + r / 4 - 1; }
 constexpr int WF16_GLOBAL_CP = 7;
 constexpr int WF16_GLOBAL_BAND = 8;
 // SEMI TAIL=TARGET reverse pass of WITH_START (start.hpp, A.stop): the forward instances keep
@@ -825,11 +823,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // a window from column 0 starts at the left boundary: H(r0 - 1, -1) (Q2; lane 0 of the
         // sweep never runs column -1, so lane 1's entry 0 is not stored)
         if (L == 0) B0a.x = (uint32_t)(pb + D * ((int32_t)r0 - 2) - (r0 <= 1 ? 0 : go + ge * ((int32_t)r0 - 1))) * 0x10001u;
-        // flags diagonal-major ([wave][lane][d = window - row group + R/4 - 1][row group]): the
-        // walk follows the diagonal, so its consecutive chunks share cache lines (window-major,
-        // every chunk it read came from a line of its own)
-        constexpr uint32_t R4 = R / 4;
-        uint4 *bf = A.bflags + ((size_t)wv * 64 + lane) * band_diags(WD, R) * R4;
+        uint4 *bf = A.bflags + ((size_t)wv * 64 + lane) * (WD / 4) * (R / 4);
         const bool any = valid[0] || valid[1];
         c = L;
         uint32_t fdummy = NN;
@@ -851,10 +845,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             bstep(3, HB, HA, B0b.z, B1a.y);
             B0a = B1a; B0b = B1b; B1a = B2a; B1b = B2b;
             if (any) {
-                uint4 *dst = bf + (t / 4 + R4 - 1) * R4;   // row group g at (t/4 - g + R4 - 1) * R4 + g
+                uint4 *dst = bf + (t / 4) * (R / 4);
 #pragma unroll
                 for (int k = 0; k < R; k += 4)
-                    dst[(k / 4) * (1 - (int)R4)] = make_uint4(__builtin_amdgcn_perm(dw[k + 1], dw[k], 0x05040100u),
+                    dst[k / 4] = make_uint4(__builtin_amdgcn_perm(dw[k + 1], dw[k], 0x05040100u),
                                             __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x05040100u),
                                             __builtin_amdgcn_perm(dw[k + 1], dw[k], 0x07060302u),
                                             __builtin_amdgcn_perm(dw[k + 3], dw[k + 2], 0x07060302u));
@@ -1313,7 +1307,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             // the band pass right behind the sweep, in the same wave: no second prologue, and the
             // checkpoints and hand-offs just written (this wave's own stores) are read from L2
             __threadfence_block();
-            asm volatile("" ::: "memory");   // nothing of the band pass hoisted above the sweep
             band_pass();
         }
     } else {
