@@ -398,7 +398,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             // band's half width w (window of lane lg: columns [max(lg*R - w, 0), + R + 2w))
             if (pl.packed16 && pl.tb && wf_algo == WF_GLOBAL && pl.R16 % 4 == 0 && env_flag("GASALX_TB_BAND", true)) {
                 const char *bw = std::getenv("GASALX_TB_BAND_W");
-                const int w = bw ? std::max(0, std::atoi(bw)) : 12;
+                const int w = bw ? std::max(0, std::atoi(bw)) : 10;   // w 8-16 within 2 % (profiles/r04/k_nw_tb_w*.json)
                 pl.tb_band = true;
                 pl.band_w = (uint32_t)w;
                 pl.band_wd = ((uint32_t)(pl.R16 + 2 * w) + 3u) & ~3u;
