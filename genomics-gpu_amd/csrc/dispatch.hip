@@ -447,7 +447,28 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         }                                                                                \
     } while (0)
 
+// threads per block of the band walk with LDS-staged regions: 128 x 50 entries x 8 B = 50 KB at
+// G16R20, w = 10, i.e. three blocks per CU
+constexpr uint32_t kTbStageBlock = 128;
 static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
+
+// Device-to-device byte copy, 16 bytes per lane (the CIGAR buffer's start as the query batch,
+// get_tb.h:94): the runtime's copy ran at ≈0.4 TB/s for the config-3 batch (30 MB, 80 us
+// under the two-stream bench, profiles/r04_nw_tb_kernel_stats.csv).  Both pointers 16-byte
+// aligned, else the runtime copy.
+__global__ __launch_bounds__(256) void copy16_kernel(uint4 *dst, const uint4 *src, uint64_t n16) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+}
+static hipError_t copy_d2d(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    if (((uintptr_t)dst | (uintptr_t)src) & 15u || bytes < 4096)
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+    const uint64_t n16 = bytes / 16;
+    copy16_kernel<<<(int)std::min<uint64_t>((n16 + 255) / 256, 8192), 256, 0, st>>>((uint4 *)dst, (const uint4 *)src, n16);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && bytes % 16)
+        e = hipMemcpyAsync((uint8_t *)dst + n16 * 16, (const uint8_t *)src + n16 * 16, bytes % 16, hipMemcpyDeviceToDevice, st);
+    return e;
+}
 
 // Launch the wavefront kernel(s) of plan `pl` over one device batch: the packed
 // kernel first when the plan has one (it flags the blocks it aligned), then the
@@ -739,7 +760,7 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     // reference where get_tb writes into unpacked_query_batch (get_tb.h:94,
     // gasal_align.cu:281); n_cigar_ops = query_batch_lens unless get_tb runs.
     if (tb && out.cigar && (const void *)out.cigar != (const void *)b.q_batch)
-        HIPCHK(hipMemcpyAsync(out.cigar, b.q_batch, b.q_bytes, hipMemcpyDeviceToDevice, st));
+        HIPCHK(copy_d2d(out.cigar, b.q_batch, b.q_bytes, st));
     const bool runs_tb = tb && (p.algo == 1 || p.algo == 3) && pl.kind != PLAN_NONE;
     if (tb && out.n_cigar_ops && !runs_tb && (const void *)out.n_cigar_ops != (const void *)b.q_lens)
         HIPCHK(hipMemcpyAsync(out.n_cigar_ops, b.q_lens, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
@@ -1189,7 +1210,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.pk_fix = ws.aux.as<int32_t>();
             T.pk_q8 = tb_q8;
         }
-        T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1;
+        T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1; T.band_lds = 0;
         T.fb_list = T.fb_count = nullptr;
         T.list = T.n_dev = nullptr;
         if (fb_count) {
@@ -1199,8 +1220,17 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.fb_count = fb_count;
             T.fb_list = fb_count + 64;
             HIPCHK(hipMemsetAsync(fb_count, 0, 4, st));
+            // lane-window regions staged in LDS (generic.hpp tb_kernel); GASALX_TB_STAGE=0: off (A/B)
+            const uint32_t nE = (pl.band_wd / 4) * (pl.R16 / 4);
+            if (env_flag("GASALX_TB_STAGE", true) && (size_t)kTbStageBlock * nE * 8 <= 160 * 1024) T.band_lds = nE;
         }
-        tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
+        if (T.band_lds) {
+            const size_t lds = (size_t)kTbStageBlock * T.band_lds * 8;
+            if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)tb_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            tb_kernel<<<grid_for(n, kTbStageBlock), kTbStageBlock, lds, st>>>(T);
+        } else {
+            tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
+        }
         HIPCHK(hipGetLastError());
         if (fb_count) {
             // pairs whose path left the band: the full-matrix packed traceback kernel over the
@@ -1220,6 +1250,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             if (rc) return rc;
             TbArgs T2 = T;
             T2.band = nullptr;
+            T2.band_lds = 0;
             T2.list = T.fb_list;
             T2.n_dev = fb_count;
             T2.slot_of = nullptr;
@@ -1303,7 +1334,8 @@ static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0,
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
     // rows x 64 lanes x 4 bytes, per problem of a lane group
     const size_t lds = (((size_t)4 * per_group * (64 / G) * A.lds_stride + 15) & ~(size_t)15) +
-                       (size_t)per_group * 4 * 4 * rows * 64 * 4;
+                       (size_t)per_group * 4 * 4 * rows * 64 * 4 +
+                       (GX_HMM_CODE16 && per_group == 1 ? (size_t)4 * (64 / G) * A.lds_stride * 2 + 16 : 0);
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
     HmmFn fn = per_group == 2 ? (quals ? (absorb ? hmm2_lookup<true, true>(G) : hmm2_lookup<true, false>(G))
                                        : (absorb ? hmm2_lookup<false, true>(G) : hmm2_lookup<false, false>(G)))

@@ -51,7 +51,10 @@ __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' |
 #define GX_HMM_PKFMA 0   // 1: the I and MM FMAs of a cell as one v_pk_fma_f32 (A/B: 4,574 vs 5,242 GCUPS, r03_pairhmm_ab.md)
 #endif
 #ifndef GX_HMM_PREFETCH
-#define GX_HMM_PREFETCH 1   // table rows one column ahead in a second register set (0: loaded in place)
+#define GX_HMM_PREFETCH 2   // 2: rows one column and bytes two ahead, fenced; 1: rows one column ahead, unfenced; 0: loaded in place
+#endif
+#ifndef GX_HMM_CODE16
+#define GX_HMM_CODE16 0   // 1: the table path reads u16 table offsets per haplotype position
 #endif
 #ifndef GX_HMM_WAVES
 #define GX_HMM_WAVES 4   // waves per SIMD the register allocator must allow (4: 128 VGPRs + 16 B of scratch, 5,551 against 5,309 GCUPS at 3, profiles/r04/pairhmm_4w.json)
@@ -157,9 +160,24 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
             }
         }
     }
+#if GX_HMM_CODE16
+    // the table offset of every haplotype position, (hb & 6) * NQ * 512, as u16 after the
+    // tables (one read and one add per column instead of a byte read, shift, mask and add)
+    const uint32_t c16_off = tbl_off + 4u * (4 * NQ * 64 * 16);
+    uint16_t *c16 = reinterpret_cast<uint16_t *>(lds + c16_off) + (size_t)wave * P * stride;
+    if (tab) {
+        for (uint32_t i = lane; i < P * stride; i += 64) c16[i] = (uint16_t)((wl[i] & 6u) * (NQ * 512u));
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint16_t *hc16 = c16 + slot * stride;
+#endif
     // rows' priors for haplotype byte hb: from the table (tab) or by compare
     auto tload = [&](uint32_t hb, float (&aa)[RR]) {
+#if GX_HMM_CODE16
+        const float4 *p = reinterpret_cast<const float4 *>(tb + hb);                         // hb: the u16 offset
+#else
         const float4 *p = reinterpret_cast<const float4 *>(tb + (hb & 6u) * (NQ * 512u));   // code * NQ * 1 KB
+#endif
 #pragma unroll
         for (int qd = 0; qd < NQ; ++qd) {
             const float4 x = p[qd * 64];
@@ -175,6 +193,14 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
     // registers (rb, qm1, qm3) are dead in the table path
     const bool bottom = lg == G - 1;
     float acc = 0.f;
+    // the table path's per-column source: u16 offsets (GX_HMM_CODE16) or haplotype bytes
+    auto tsrc = [&](uint32_t j) -> uint32_t {
+#if GX_HMM_CODE16
+        return hc16[j];
+#else
+        return hap[j];
+#endif
+    };
     auto sweep = [&](auto tabc) {
         constexpr bool TABP = decltype(tabc)::value;
         uint32_t hmax = H;
@@ -218,7 +244,7 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
             else { MU = rM; IU = rI; DU = rD; }
             if (valid && j >= 0 && (uint32_t)j < H) {
                 float aa[RR];
-                if constexpr (TABP) tload(hap[j], aa);
+                if constexpr (TABP) tload(tsrc(j), aa);
                 else cload(hap[j], aa);
                 column(aa, MU, IU, DU);
                 if (bottom) acc = __fadd_rn(acc, __fadd_rn(MU, IU));       // row R-1, column j (:166-167)
@@ -246,19 +272,44 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
                 // (8 VGPRs fewer; the other waves of the SIMD cover the LDS latency)
                 for (uint32_t s = s1; s < hmin; ++s) {
                     float aa[RR];
-                    tload(hap[s - lg], aa);
+                    tload(tsrc(s - lg), aa);
                     steady(aa);
                 }
+            } else if constexpr (TABP && GX_HMM_PREFETCH == 2) {
+                // table rows one column ahead and haplotype bytes two ahead, pinned in place
+                // by scheduling fences: left to itself the scheduler sinks the loads next to
+                // their first use (the row read then waits on the byte read, and the column on
+                // the row read).  Loop bounds are wave-uniform (SGPR loop).  Byte reads past a
+                // pair's columns (up to column hmin + 1) stay inside the slot + table region
+                // and are not used.
+                const uint32_t he = __builtin_amdgcn_readfirstlane(hmin);
+                float aaA[RR], aaB[RR];
+                uint32_t s = __builtin_amdgcn_readfirstlane(s1);
+                uint32_t hbn = 0;
+                if (s < he) { tload(tsrc(s - lg), aaA); hbn = tsrc(s + 1 - lg); }
+                for (; s + 1 < he; s += 2) {
+                    tload(hbn, aaB);
+                    hbn = tsrc(s + 2 - lg);
+                    __builtin_amdgcn_sched_barrier(0);
+                    steady(aaA);
+                    __builtin_amdgcn_sched_barrier(0);
+                    tload(hbn, aaA);
+                    hbn = tsrc(s + 3 - lg);
+                    __builtin_amdgcn_sched_barrier(0);
+                    steady(aaB);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (s < he) steady(aaA);
             } else if constexpr (TABP) {
                 // table rows one step ahead, two register sets in turn (hap reads past a
                 // pair's columns stay inside the slot + table region and are not used)
                 float aaA[RR], aaB[RR];
                 uint32_t s = s1;
-                if (s < hmin) tload(hap[s - lg], aaA);
+                if (s < hmin) tload(tsrc(s - lg), aaA);
                 for (; s + 1 < hmin; s += 2) {
-                    tload(hap[s + 1 - lg], aaB);
+                    tload(tsrc(s + 1 - lg), aaB);
                     steady(aaA);
-                    tload(hap[s + 2 - lg], aaA);
+                    tload(tsrc(s + 2 - lg), aaA);
                     steady(aaB);
                 }
                 if (s < hmin) steady(aaA);

@@ -1,5 +1,6 @@
 #!/bin/bash
-# round 4, session L: PairHMM with fenced table / byte prefetch (GX_HMM_PREFETCH=2).
+# round 4, session L: PairHMM with fenced table / byte prefetch (GX_HMM_PREFETCH=2); A/B against
+# u16 table offsets (c16) and the unfenced prefetch (pf1).
 # Output: gpurun_out/r04l/
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
@@ -27,5 +28,8 @@ PY
 PYT="python -u -m pytest -m gpu -q --timeout 120 --timeout-method thread"
 step hmmtests 600 $PYT tests/ -k "hmm"
 run pairhmm "X=1" pairhmm --steps 10 --parity-pairs 100000
+V=$ROOT/genomics-gpu_amd/lib/variants
+run pairhmm_c16 "GASALX_LIB=$V/libgasal_c16.so" pairhmm --steps 10 --parity-pairs 100000
+run pairhmm_pf1 "GASALX_LIB=$V/libgasal_pf1.so" pairhmm --steps 10 --parity-pairs 1000
 run pairhmm_b "X=1" pairhmm --steps 10 --parity-pairs 1000
 exit 0
