@@ -447,9 +447,6 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
         }                                                                                \
     } while (0)
 
-// threads per block of the band walk with LDS-staged regions: 128 x 50 entries x 8 B = 50 KB at
-// G16R20, w = 10, i.e. three blocks per CU
-constexpr uint32_t kTbStageBlock = 128;
 static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
 
 // Device-to-device byte copy, 16 bytes per lane (the CIGAR buffer's start as the query batch,
@@ -1210,7 +1207,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.pk_fix = ws.aux.as<int32_t>();
             T.pk_q8 = tb_q8;
         }
-        T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1; T.band_lds = 0;
+        T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1;
         T.fb_list = T.fb_count = nullptr;
         T.list = T.n_dev = nullptr;
         if (fb_count) {
@@ -1220,17 +1217,8 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.fb_count = fb_count;
             T.fb_list = fb_count + 64;
             HIPCHK(hipMemsetAsync(fb_count, 0, 4, st));
-            // lane-window regions staged in LDS (generic.hpp tb_kernel); GASALX_TB_STAGE=0: off (A/B)
-            const uint32_t nE = (pl.band_wd / 4) * (pl.R16 / 4);
-            if (env_flag("GASALX_TB_STAGE", true) && (size_t)kTbStageBlock * nE * 8 <= 160 * 1024) T.band_lds = nE;
         }
-        if (T.band_lds) {
-            const size_t lds = (size_t)kTbStageBlock * T.band_lds * 8;
-            if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)tb_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            tb_kernel<<<grid_for(n, kTbStageBlock), kTbStageBlock, lds, st>>>(T);
-        } else {
-            tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
-        }
+        tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
         HIPCHK(hipGetLastError());
         if (fb_count) {
             // pairs whose path left the band: the full-matrix packed traceback kernel over the
@@ -1250,7 +1238,6 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             if (rc) return rc;
             TbArgs T2 = T;
             T2.band = nullptr;
-            T2.band_lds = 0;
             T2.list = T.fb_list;
             T2.n_dev = fb_count;
             T2.slot_of = nullptr;

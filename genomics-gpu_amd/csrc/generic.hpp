@@ -590,10 +590,6 @@ struct TbArgs {
     // the CIGAR the full-matrix walk writes later)
     const uint4 *band;
     uint32_t band_w, band_wd, pk_ppw;   // pk_ppw: pairs (slots) per wave of the DP launch
-    // band_lds: entries of one lane window region, (band_wd / 4) * (R / 4), when the walk stages
-    // each region it enters in its own LDS slot (dynamic LDS, blockDim x band_lds uint2); 0: reads
-    // every chunk from global memory
-    uint32_t band_lds;
     uint32_t *fb_list, *fb_count;
     // fallback walk: thread tid walks pair list[tid], tid < *n_dev; its slot in the DP launch is tid
     const uint32_t *list, *n_dev;
@@ -607,23 +603,6 @@ __device__ __forceinline__ uint32_t tb_code(const uint8_t *seq, uint32_t off, ui
         key = k;
         v = packed ? make_uint2(reinterpret_cast<const uint32_t *>(seq)[(off >> 3) + (uint32_t)k], 0u)
                    : *reinterpret_cast<const uint2 *>(seq + off + 8u * (uint32_t)k);
-    }
-    const uint32_t p = pos & 7u;
-    return packed ? (v.x >> (28 - 4 * p)) & 15u : ((p < 4 ? v.x : v.y) >> (8 * (p & 3u))) & 15u;
-}
-// the same with the next block down (the walk's positions only decrease) loaded one block
-// ahead, so the walk does not wait on a sequence load at each block boundary
-__device__ __forceinline__ uint32_t tb_code_pf(const uint8_t *seq, uint32_t off, uint32_t pos, int packed, uint2 &v,
-                                               int32_t &key, uint2 &pv, int32_t &pkey) {
-    const int32_t k = (int32_t)(pos >> 3);
-    auto ld = [&](int32_t kk) {
-        return packed ? make_uint2(reinterpret_cast<const uint32_t *>(seq)[(off >> 3) + (uint32_t)kk], 0u)
-                      : *reinterpret_cast<const uint2 *>(seq + off + 8u * (uint32_t)kk);
-    };
-    if (k != key) {
-        v = k == pkey ? pv : ld(k);
-        key = k;
-        if (k > 0) { pv = ld(k - 1); pkey = k - 1; }
     }
     const uint32_t p = pos & 7u;
     return packed ? (v.x >> (28 - 4 * p)) & 15u : ((p < 4 ? v.x : v.y) >> (8 * (p & 3u))) & 15u;
@@ -652,9 +631,6 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                                       ((A.band_wd / 4) * (A.pk_R / 4)) * 2 + (slot & 1u)
                             : nullptr;
     bool out_of_band = false;
-    extern __shared__ uint2 tb_region[];
-    uint2 *my_region = tb_region + (size_t)threadIdx.x * A.band_lds;
-    int32_t reg_lane = -1;
     // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
     // pair at 8 * c + (tid & 7)
     const bool il8 = pk && A.pk_q8;
@@ -677,8 +653,6 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int64_t chunk_key = -1;
     uint2 qv = make_uint2(0u, 0u), tv = make_uint2(0u, 0u);
     int32_t qkey = -1, tkey = -1;
-    uint2 qpv = make_uint2(0u, 0u), tpv = make_uint2(0u, 0u);
-    int32_t qpkey = -1, tpkey = -1;
     while (i >= 0 && j >= 0) {
         // get_tb.h:50-71: linear cell index over (strip, row, column); a start
         // one row past the padded query (j == q8) wraps to row 0 of the next strip
@@ -694,41 +668,15 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                 const int32_t L = max((int32_t)(lane * A.pk_R) - (int32_t)A.band_w, 0);
                 const uint32_t t = (uint32_t)((int32_t)col - L);
                 if (t >= A.band_wd) { out_of_band = true; break; }
-                if (A.band_lds) {
-                    // the path crosses each lane's window once, top to bottom: on entering one, its
-                    // region (this pair's half of every entry) is read with all loads in flight and
-                    // kept in LDS, so the walk waits on HBM once per lane instead of once per chunk
-                    if ((int32_t)lane != reg_lane) {
-                        reg_lane = (int32_t)lane;
-                        const uint32_t nE = A.band_lds;
-                        const uint2 *src = bnd2 + (uint64_t)lane * nE * 2;
-                        for (uint32_t e0 = 0; e0 < nE; e0 += 16) {
-                            uint2 v[16];
-#pragma unroll
-                            for (int u = 0; u < 16; ++u) v[u] = e0 + u < nE ? src[(uint64_t)(e0 + u) * 2] : make_uint2(0u, 0u);
-#pragma unroll
-                            for (int u = 0; u < 16; ++u)
-                                if (e0 + u < nE) my_region[e0 + u] = v[u];
-                        }
-                        chunk_key = -1;
-                    }
-                    const int64_t e = (int64_t)(t >> 2) * (A.pk_R / 4) + (k >> 2);
-                    if (e != chunk_key) {
-                        const uint2 c2 = my_region[e];
-                        chunk = make_uint4(c2.x, c2.y, 0u, 0u);
-                        chunk_key = e;
-                    }
-                } else {
-                    const int64_t key = (((int64_t)lane * (A.band_wd / 4) + (t >> 2)) * (A.pk_R / 4) + (k >> 2)) * 2;
-                    if (key != chunk_key) {
-                        const uint2 c2 = bnd2[key];
-                        chunk = make_uint4(c2.x, c2.y, 0u, 0u);
-                        chunk_key = key;
-                    }
+                const int64_t key = (((int64_t)lane * (A.band_wd / 4) + (t >> 2)) * (A.pk_R / 4) + (k >> 2)) * 2;
+                if (key != chunk_key) {
+                    const uint2 c2 = bnd2[key];
+                    chunk = make_uint4(c2.x, c2.y, 0u, 0u);
+                    chunk_key = key;
                 }
                 const uint32_t fl = (((k & 2u) ? chunk.y : chunk.x) >> (16 * (k & 1u) + (t & 3u))) & 0xFFFFu;
-                const uint32_t qc = tb_code_pf(A.qseq, qoff, row, A.seq_packed, qv, qkey, qpv, qpkey);
-                const uint32_t tc = tb_code_pf(A.tseq, toff, col, A.seq_packed, tv, tkey, tpv, tpkey);
+                const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
+                const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
                 if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
                 const uint32_t u = fix_diag ? 0u : (fl & 1u);
@@ -753,8 +701,8 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                     chunk_key = key;
                 }
                 const uint32_t fl = (((k & 2u) ? chunk.y : chunk.x) >> (16 * (k & 1u) + (s & 3u))) & 0xFFFFu;
-                const uint32_t qc = tb_code_pf(A.qseq, qoff, row, A.seq_packed, qv, qkey, qpv, qpkey);
-                const uint32_t tc = tb_code_pf(A.tseq, toff, col, A.seq_packed, tv, tkey, tpv, tpkey);
+                const uint32_t qc = tb_code(A.qseq, qoff, row, A.seq_packed, qv, qkey);
+                const uint32_t tc = tb_code(A.tseq, toff, col, A.seq_packed, tv, tkey);
                 int32_t sc = qc == tc ? A.a : -A.b;                                   // global.h rule
                 if (A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = -A.npen;
                 if (A.is_local && !A.has_npen && ((int32_t)qc == A.nval || (int32_t)tc == A.nval)) sc = 0;   // local N rule
