@@ -59,7 +59,7 @@ WORKLOADS = {
                      label="config2: SW local affine (a1 b4 o6 e1) score+ends, 1M pairs x 150bp per GPU, "
                            "seed 0x5EED0002"),
     "sw_local_start": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL, start_pos=G.WITH_START),
-                           bytes=340, ops=12,
+                           bytes=340, ops=12, streams=2,
                            label="config2 + WITH_START: SW local score+ends+starts, 1M pairs x 150bp per GPU"),
     "sw_local_tb": dict(kind=2, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL, start_pos=G.WITH_TB),
                         bytes=340 + 152, ops=16, streams=2,
@@ -71,14 +71,14 @@ WORKLOADS = {
                      label="config-3 data, NW global score only (no traceback), 100K pairs x 300bp per GPU: the "
                            "sweep the band traceback's first pass is built on"),
     "nw_tb": dict(kind=3, pairs=100_000, scaling="weak", params=dict(algo=G.GLOBAL, start_pos=G.WITH_TB), bytes=650,
-                  ops=16, streams=2, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
+                  ops=16, streams=3, label="config3: NW global + traceback/CIGAR, 100K pairs x 300bp per GPU, seed 0x5EED0003"),
     "semi": dict(kind=4, pairs=10_000_000, scaling="strong",
                  params=dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET), bytes=364, ops=11,
                  label="config4: semi-global TARGET/TARGET, 10M 150bp reads in 182bp windows sharded over the "
                        "GPUs, RCCL gather of scores, seed 0x5EED0004"),
     "semi_start": dict(kind=4, pairs=10_000_000, scaling="strong",
                        params=dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET, start_pos=G.WITH_START,
-                                   max_query_len=192), bytes=372, ops=11,
+                                   max_query_len=192), bytes=372, ops=11, streams=2,
                        label="config4 + WITH_START: semi-global TARGET/TARGET score+ends+starts, 10M reads sharded"),
     "semi_banded": dict(kind=4, pairs=10_000_000, scaling="strong", params=dict(algo=G.BANDED, k_band=16), bytes=364,
                         ops=None, label="config4 data, banded-tiled k_band=16 (SURVEY §8(d) second run), 10M reads "
@@ -130,8 +130,10 @@ def parse():
     ap.add_argument("--streams", type=int, default=None,
                     help="GASAL workloads: engines (gasal_gpu_storage) on their own streams, steps "
                          "issued round-robin as the reference's host program drives gasal_aln_async "
-                         "(test_prog.cpp NB_STREAMS = 2); 1 = every step on one stream.  Default: 2 for "
-                         "the traceback workloads (a step's walk runs beside the next step's DP), else 1")
+                         "(test_prog.cpp NB_STREAMS = 2 per host thread); 1 = every step on one stream.  Default: "
+                         "2 for the traceback and WITH_START workloads (a step's walk or reverse-pass prep runs "
+                         "beside the next step's DP), 3 for config 3 (profiles/r04/p_nw_tb_s*.json: 2 -> 3,860, "
+                         "3 -> 4,189, 4 -> 3,727 GCUPS in one session), else 1")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline timings")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-staged (PCIe-inclusive) timing")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave out the all-gather of scores")
