@@ -560,6 +560,9 @@ def run_cpu_plumbing(args, wl):
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "int32", "data": "synthetic (SURVEY.md 8(d) config 1 generator)",
            "config": {"workload": wl["label"], "pairs": n, "cells_per_step": cells, "cores": 1}}
+    # this workload is the CPU path itself: its baseline is the same timing, stated like every other line's
+    out["cpu_baseline"] = {"value": out["value"], "unit": "GCUPS", "cores": 1, "kind": "port",
+                           "sample": f"the whole workload ({n} pairs x {args.steps} passes, 1 thread)"}
     if torch.cuda.is_available():
         eng = G.Engine(0)
         g = eng.align_host(batch, G.make_params(**pkw), fields=["score", "q_end", "t_end"])
