@@ -54,7 +54,10 @@ __device__ __forceinline__ bool acgt(uint32_t b) { return b == 'A' || b == 'C' |
 #define GX_HMM_PREFETCH 2   // 2: rows one column and bytes two ahead, fenced; 1: rows one column ahead, unfenced; 0: loaded in place
 #endif
 #ifndef GX_HMM_CODE16
-#define GX_HMM_CODE16 0   // 1: the table path reads u16 table offsets per haplotype position
+#define GX_HMM_CODE16 0   // 1: the table path reads u16 table offsets per haplotype position (5,320 against 5,593: the extra LDS takes a block per CU)
+#endif
+#ifndef GX_HMM_MASKB
+#define GX_HMM_MASKB 0   // 1: the table path's staged bytes masked to (hb & 6) once, one shift per column
 #endif
 #ifndef GX_HMM_WAVES
 #define GX_HMM_WAVES 4   // waves per SIMD the register allocator must allow (4: 128 VGPRs + 16 B of scratch, 5,551 against 5,309 GCUPS at 3, profiles/r04/pairhmm_4w.json)
@@ -160,6 +163,14 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
             }
         }
     }
+#if GX_HMM_MASKB
+    // table path: the staged bytes reduced to their code bits, (hb & 6), so a column's table
+    // offset is one shift (this wave's own slots; the compare path keeps the bytes)
+    if (tab) {
+        for (uint32_t i = lane; i < P * stride; i += 64) wl[i] &= 6u;
+        __builtin_amdgcn_wave_barrier();
+    }
+#endif
 #if GX_HMM_CODE16
     // the table offset of every haplotype position, (hb & 6) * NQ * 512, as u16 after the
     // tables (one read and one add per column instead of a byte read, shift, mask and add)
@@ -175,6 +186,8 @@ __global__ __launch_bounds__(256, GX_HMM_WAVES) void pairhmm_kernel(HmmArgs A) {
     auto tload = [&](uint32_t hb, float (&aa)[RR]) {
 #if GX_HMM_CODE16
         const float4 *p = reinterpret_cast<const float4 *>(tb + hb);                         // hb: the u16 offset
+#elif GX_HMM_MASKB
+        const float4 *p = reinterpret_cast<const float4 *>(tb + hb * (NQ * 512u));          // hb = code bits
 #else
         const float4 *p = reinterpret_cast<const float4 *>(tb + (hb & 6u) * (NQ * 512u));   // code * NQ * 1 KB
 #endif
