@@ -120,7 +120,11 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warmup steps (default: at least 3 steps and at least --warmup-seconds of GPU "
+                         "time, so the timed steps run at the clock the GPU settles at under load: a cold "
+                         "MI355X ramps over the first ~30 ms, profiles/r05/clock_ramp.md)")
+    ap.add_argument("--warmup-seconds", type=float, default=0.5)
     ap.add_argument("--pairs", type=int, default=0,
                     help="pairs per GPU (weak workloads) or global pairs (strong); default: the config's")
     ap.add_argument("--workload", default="sw_local", choices=sorted(WORKLOADS))
@@ -549,14 +553,14 @@ def run_cpu_plumbing(args, wl):
     batch = G.Batch.synth(1, n, SEEDS[1])
     pkw = wl["params"]
     cells = cells_of(batch)
-    for _ in range(args.warmup):
+    for _ in range(3 if args.warmup is None else args.warmup):
         oracle_align(O, batch, pkw, 1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         o = oracle_align(O, batch, pkw, 1)
     dt = time.perf_counter() - t0
     out = {"metric": METRICS["cpu_plumbing"], "value": round(cells * args.steps / dt / 1e9, 4), "unit": "GCUPS",
-           "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "n_gpus": 1, "steps": args.steps, "warmup": 3 if args.warmup is None else args.warmup,
            "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "int32", "data": "synthetic (SURVEY.md 8(d) config 1 generator)",
            "config": {"workload": wl["label"], "pairs": n, "cells_per_step": cells, "cores": 1}}
@@ -765,8 +769,24 @@ def main():
             with torch.cuda.stream(sets[k][1]):
                 sets[k][2]()
 
-    for i in range(args.warmup):
-        step(i)
+    if args.warmup is not None:
+        for i in range(args.warmup):
+            step(i)
+    else:
+        # time-based: every rank warms for the same number of steps (the max over ranks)
+        i, t_w = 0, time.perf_counter()
+        while i < 3 or time.perf_counter() - t_w < args.warmup_seconds:
+            step(i)
+            i += 1
+            if i >= 3:
+                torch.cuda.synchronize(dev)
+        wt = torch.tensor([i], dtype=torch.int64, device=dev)
+        if world > 1:
+            wt = allreduce(wt, dist.ReduceOp.MAX)
+        while i < int(wt[0]):
+            step(i)
+            i += 1
+        args.warmup = i
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -14,7 +14,7 @@ for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST
             "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-e2e "$@" > "$OUT/p$i.json" 2> "$OUT/p$i.err"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $pass --output-format csv -d "$OUT/p$i" -o run -- python3 "$ROOT/bench.py" --steps 3 --no-cpu --no-e2e "$@" > "$OUT/p$i.json" 2> "$OUT/p$i.err"
   rc=$?; echo "pass $i rc=$rc ($pass)"
   if fatal $rc; then exit $rc; fi
 done
