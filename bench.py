@@ -980,6 +980,29 @@ def main():
                          "kernel": pmc.get("kernel"), "kernel_ms_pmc": round(pk_t * 1e3, 4),
                          "source": f"profiles/pmc_{args.workload}.json (SQ_INSTS_VALU; same library sha256 and "
                                    f"plan as this run)"})
+            cen = pmc.get("census")
+            if cen and cen.get("cycles_per_valu"):
+                # per-class issue bound: the same instruction count priced by the
+                # steady loop's mix at the measured issue costs (kernel_census.py: full-rate ops 2.07
+                # cycles, VOP3P / v_perm / three-input VOP3 4.1-4.25 per wave64 instruction per SIMD)
+                cpv = float(cen["cycles_per_valu"])
+                t_priced = vi * cpv / (SIMDS * CLOCK)
+                valu["issue_priced"] = {
+                    "frac": round(t_priced / pk_t, 4), "cycles_per_valu": cpv,
+                    "loop_valu": cen.get("loop_valu"), "loop_issue_cycles": cen.get("loop_issue_cycles"),
+                    "basis": "PMC SQ_INSTS_VALU x the steady loop's average issue cost per VALU instruction "
+                             "(tools/kernel_census.py over this library, profiles/r04_valu_issue_rates.json), "
+                             "against 1,024 SIMDs x 2.4 GHz: how close the kernel runs to the issue bound of its "
+                             "own instruction mix ('frac' beside it prices every instruction at 2 cycles)"}
+        if kind != 5 and wl["ops"]:
+            # fixed ceiling: SURVEY.md 8(d)'s algorithmic ops per cell at the packed
+            # 2 x 16-bit lane rate, independent of how many instructions the kernel issues
+            fixed = 2 * VALU_LANE_OPS / wl["ops"]
+            valu["fixed_ceiling"] = {
+                "peak": round(fixed / 1e12, 4), "unit": "T cells/s", "frac": round(kcells / fixed, 4),
+                "basis": f"{wl['ops']} algorithmic int ops per cell (SURVEY.md 8(d)) at 2 x 16-bit lanes per "
+                         f"32-bit lane op, 78.6 T lane ops/s (MI355X_MICROARCH.md): a ceiling that does not "
+                         f"move with the kernel's own instruction count"}
         out = {
             "metric": METRICS.get(args.workload, MAIN_METRIC),
             "value": round(gcups, 2),

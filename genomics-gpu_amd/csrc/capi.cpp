@@ -300,7 +300,7 @@ int align_host_pipelined(gasalx_engine *eng, const gasalx_params *params, const 
         shape.max_q = mq;
         shape.max_t = mt;
         shape.sort = gx::uneven_lengths(*params, hb->q_lens + i0, hb->t_lens + i0, m);
-        shape.one_t8 = gx::one_pad8(hb->t_lens + i0, m);
+        shape.one_t8 = gx::one_pad8(hb->t_lens + i0, m, shape.max_t);
         shape.tb_split = false;   // the two slots' streams already overlap one chunk's walk with the next DP
         if ((rc = gx::align_device(s.ws, *params, db, dout, s.st, shape))) {
             for (HostSlot &x : eng->slot) (void)hipStreamSynchronize(x.st);
@@ -383,7 +383,7 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     shape.max_q = db.max_q_len;
     shape.max_t = db.max_t_len;
     shape.sort = gx::uneven_lengths(*params, hb->q_lens, hb->t_lens, n);
-    shape.one_t8 = gx::one_pad8(hb->t_lens, n);
+    shape.one_t8 = gx::one_pad8(hb->t_lens, n, shape.max_t);
     rc = gx::align_device(eng->ws, *params, db, dout, st, shape);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
 #define BACK(h, d, cnt)                                                                             \
@@ -678,3 +678,28 @@ int gasalx_host_free(void *p) {
 }
 
 }  // extern "C"
+
+// Diagnostics (gasalx.h): the last packed launch's "aligned here" flags of each workspace.
+extern "C" int gasalx_packed_pairs(gasalx_engine *e, uint64_t *handled, uint64_t *total) {
+    if (!e || !handled || !total) { gx::set_error("gasalx_packed_pairs: NULL argument"); return GASALX_EINVAL; }
+    *handled = *total = 0;
+    CK(hipSetDevice(e->device));
+    auto one = [&](gx::Workspace &ws, hipStream_t st) -> int {
+        if (st) CK(hipStreamSynchronize(st));
+        if (!ws.pk_flags || !ws.misc.p) return GASALX_OK;
+        std::vector<uint8_t> f(ws.pk_flags);
+        CK(hipMemcpy(f.data(), ws.misc.p, f.size(), hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < ws.pk_flags; i++) {
+            const uint64_t lo = (uint64_t)i * ws.pk_ppb, hi = std::min<uint64_t>(lo + ws.pk_ppb, ws.pk_pairs);
+            if (hi > lo && f[i]) *handled += hi - lo;
+        }
+        *total += ws.pk_pairs;
+        ws.pk_flags = 0;   // read once: the next call counts only launches after this one
+        return GASALX_OK;
+    };
+    int rc;
+    if ((rc = one(e->ws, e->stream))) return rc;
+    for (HostSlot &s : e->slot)
+        if ((rc = one(s.ws, s.st))) return rc;
+    return GASALX_OK;
+}

@@ -44,8 +44,8 @@ void Workspace::release_all() {
     sides.clear();
     for (hipEvent_t *x : {&fork, &join, &dp_done})
         if (*x) { (void)hipEventDestroy(*x); *x = nullptr; }
-    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux, &rev_q,
-                      &rev_t, &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb, &kseg}) b->release();
+    for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux,
+                      &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb, &kseg}) b->release();
 }
 
 // ----------------------------------------------------------------------------
@@ -448,6 +448,12 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     } while (0)
 
 static int grid_for(uint32_t n, uint32_t per_block) { return (int)((n + per_block - 1) / per_block); }
+// the int32 wavefront kernel's grid: every block, or, as the fallback of a packed launch (A.skip:
+// usually few or no declined blocks), at most 8 blocks per CU walking the rest (wavefront.hpp wf_kernel)
+static int wf_grid(uint32_t n, int G, bool fallback) {
+    const int g = grid_for(n, kWavesPerBlock * (64 / G));
+    return fallback ? std::min(g, 8 * 256) : g;
+}
 
 // Device-to-device byte copy, 16 bytes per lane (the CIGAR buffer's start as the query batch,
 // get_tb.h:94): the runtime's copy ran at ≈0.4 TB/s for the config-3 batch (30 MB, 80 us
@@ -492,6 +498,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         const uint32_t grid16 = grid_for(n, ppb16);
         HIPCHK(ws.misc.reserve(grid16 + 64));
         P16.handled = ws.misc.as<uint8_t>();
+        ws.pk_flags = grid16; ws.pk_ppb = ppb16; ws.pk_pairs = n;
         if (pl.tb) {
             HIPCHK(ws.aux.reserve((size_t)n * 4));
             P16.tbfix = ws.aux.as<int32_t>();
@@ -532,7 +539,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
     if (pl.lds_bytes > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
-    hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
+    hipLaunchKernelGGL(fn, dim3(wf_grid(n, pl.G, A.skip != nullptr)), dim3(kBlock), pl.lds_bytes, st, A);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }
@@ -579,6 +586,7 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     }
     HIPCHK(ws.misc.reserve(n + 64));
     HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));            // slots no class launch covers stay declined
+    ws.pk_flags = n; ws.pk_ppb = 1; ws.pk_pairs = n;
     WfArgs P16 = A;
     P16.lds_stride = pl.lds16_stride;
     P16.fast16 = 1;
@@ -605,7 +613,7 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
     if (pl.lds_bytes > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
-    hipLaunchKernelGGL(fn, dim3(grid_for(n, kWavesPerBlock * (64 / pl.G))), dim3(kBlock), pl.lds_bytes, st, A);
+    hipLaunchKernelGGL(fn, dim3(wf_grid(n, pl.G, A.skip != nullptr)), dim3(kBlock), pl.lds_bytes, st, A);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }
@@ -622,49 +630,34 @@ __global__ __launch_bounds__(256) void semi_tail_none_kernel(int32_t *score, int
     if (tend) tend[i] = (int32_t)qlen[i];
 }
 
-// WITH_START on the wavefront kernels (start.hpp): reversed slots sorted by
-// reversed target length, the same kernel over them, and the map of its ends to
-// the start cell.
+// WITH_START on the wavefront kernels (start.hpp): the same kernel reading the forward
+// sequences backwards over slots sorted by reversed target length, and the map of its ends
+// to the start cell.
 static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const uint8_t *q, const uint8_t *t,
                          int packed, const gasalx_batch &b, const BatchShape &shape, const int32_t *score,
                          const int32_t *qend, const int32_t *tend, int32_t *qstart, int32_t *tstart, hipStream_t st) {
     const uint32_t n = b.n_alns;
     const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t), t8w = t8 / 8;
-    HIPCHK(ws.rev_q.reserve((size_t)n * q8 + 64));
-    HIPCHK(ws.rev_t.reserve((size_t)n * t8 + 64));
-    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 9 + (size_t)(t8w + 1) * 8 + 64));
+    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 6 + (size_t)(t8w + 1) * 8 + 64));
     uint32_t *meta = ws.rev_meta.as<uint32_t>();
-    int32_t *rscore = reinterpret_cast<int32_t *>(meta + 4 * (size_t)n);
+    uint32_t *rqlen = meta, *rtlen = meta + n;
+    int32_t *rscore = reinterpret_cast<int32_t *>(meta + 2 * (size_t)n);
     int32_t *rqend = rscore + n, *rtend = rscore + 2 * (size_t)n;
-    uint32_t *perm = meta + 7 * (size_t)n;
-    int32_t *stop = reinterpret_cast<int32_t *>(meta + 8 * (size_t)n);
-    uint32_t *hist = meta + 9 * (size_t)n, *cursor = hist + t8w + 1;
+    uint32_t *perm = meta + 5 * (size_t)n;
+    uint32_t *hist = meta + 6 * (size_t)n, *cursor = hist + t8w + 1;
     // counting sort of the pairs by reversed target words (longest first)
     const size_t sh = (size_t)(t8w + 1) * 4;
     if (2 * sh > 64 * 1024) { set_error("WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
     HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-    // LOCAL: slots that stop early (the drift sweep's lstop) share waves (start.hpp rev_bucket);
-    // GASALX_START_STOP=0 keeps the full reverse rectangle and the length order (A/B)
-    const bool lstop = mode == REV_LOCAL && env_flag("GASALX_START_STOP", true);
+    // LOCAL: slots that stop early (the drift sweep's lstop) share waves (start.hpp rev_bucket)
+    const bool lstop = mode == REV_LOCAL;
     const int32_t *skey = lstop ? score : nullptr;
     rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match);
     rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
     rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm, nullptr,
                                                               skey, p.match);
-    HIPCHK(hipGetLastError());
-    RevArgs R;
-    R.q = q; R.t = t; R.qoff = b.q_offsets; R.toff = b.t_offsets; R.qlen = b.q_lens; R.tlen = b.t_lens;
-    R.qend = qend; R.tend = tend; R.score = score;
-    R.rq = ws.rev_q.as<uint8_t>(); R.rt = ws.rev_t.as<uint8_t>();
-    R.rqoff = meta; R.rtoff = meta + n; R.rqlen = meta + 2 * (size_t)n; R.rtlen = meta + 3 * (size_t)n;
-    R.stop = (mode == REV_SEMI || lstop) ? stop : nullptr;   // the forward score per slot
-    R.n = n; R.q8w = q8 / 8; R.t8w = t8w; R.packed = packed; R.mode = mode;
-    R.fill = 0x01010101u * (uint32_t)(p.n_code & 0xFF);
-    R.nval = (uint32_t)(p.n_code & 0xF);
-    R.perm = perm;
-    const uint64_t items = (uint64_t)n * (R.q8w + R.t8w);
-    rev_len_kernel<<<grid_for(n, 256), 256, 0, st>>>(R);
-    rev_prep_kernel<<<(unsigned)((items + 255) / 256), 256, 0, st>>>(R);
+    rev_len_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, q, b.q_offsets, b.q_lens, b.t_lens, qend, tend, packed,
+                                                      (uint32_t)(p.n_code & 0xF), n, rqlen, rtlen);
     HIPCHK(hipGetLastError());
     gasalx_params pr = p;
     pr.start_pos = 0;
@@ -673,17 +666,19 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     if (pl.kind != PLAN_WAVEFRONT) { set_error("reverse pass has no wavefront plan"); return GASALX_EUNSUPPORTED; }
     WfArgs A;
     std::memset(&A, 0, sizeof(A));
-    A.q = R.rq; A.t = R.rt;
-    A.qoff = R.rqoff; A.toff = R.rtoff; A.qlen = R.rqlen; A.tlen = R.rtlen;
+    A.q = q; A.t = t;
+    A.qoff = b.q_offsets; A.toff = b.t_offsets; A.qlen = rqlen; A.tlen = rtlen;
+    A.rev = 1;
+    A.perm = perm;
     A.score = rscore; A.qend = rqend; A.tend = rtend;
-    A.stop = mode == REV_SEMI ? R.stop : nullptr;
-    A.lstop = lstop ? R.stop : nullptr;
+    A.stop = mode == REV_SEMI ? score : nullptr;     // the forward score per pair
+    A.lstop = lstop ? score : nullptr;
     A.n = n;
-    A.packed = 0;
+    A.packed = packed;
     int rc = launch_wavefront(ws, pl, pr, A, st);
     if (rc) return rc;
-    start_map_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, perm, score, b.q_lens, R.rqlen, b.t_lens, tend, rscore,
-                                                        rqend, rtend, qstart, tstart, n);
+    start_map_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, score, b.q_lens, rqlen, b.t_lens, tend, rscore, rqend,
+                                                        rtend, qstart, tstart, n);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }
@@ -1002,10 +997,6 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st, shape.one_t8) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
         if (wf_start && dp) {
-            if ((uint64_t)n * std::max(pad8(shape.max_q), pad8(shape.max_t)) >= (1ull << 32)) {
-                set_error("WITH_START: batch too large for one call (reversed slots exceed 4 GB)");
-                return GASALX_ERANGE;
-            }
             rc = start_reverse(ws, p.algo == 3 ? REV_LOCAL : REV_SEMI, p, qsrc, tsrc, packed, b, shape, out.aln_score,
                                qend, tend, out.q_start, out.t_start, st);
             if (rc) return rc;

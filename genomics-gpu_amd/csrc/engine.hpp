@@ -32,11 +32,14 @@ struct Workspace {
     DevBuf ends_q, ends_t;          // LOCAL WITH_TB ends when the caller did not ask for them
     DevBuf misc;                    // packed kernels: per-block "aligned here" flags
     DevBuf aux;                     // packed GLOBAL+TB: H' of the traceback start cell per pair
-    DevBuf rev_q, rev_t, rev_meta;  // WITH_START: reversed slots, their offsets/lengths, reverse results
+    DevBuf rev_meta;                // WITH_START: reversed lengths, slot order, reverse-pass results
     DevBuf sort_meta;               // length sort of the forward pass: perm, inverse, histogram
     DevBuf band_cp, band_stm, band_fl;   // GLOBAL+TB band recomputation: checkpoints, hand-offs, flags
     DevBuf band_fb;                 // its fallback: count, then the list of pairs, then the launch's flags
     DevBuf kseg;                    // packed LOCAL keys by segments: the finished segments' keys per wave
+    // the last packed launch's "aligned here" flags in misc (gasalx_packed_pairs): flag count, pairs
+    // per flag, pairs of the launch (0 flags: no packed launch yet)
+    uint32_t pk_flags = 0, pk_ppb = 0, pk_pairs = 0;
     // traceback batches in chunks (align_device, GASALX_TB_CHUNKS): DPs on the
     // caller's stream, walks on walk_stream; one workspace per further chunk; all
     // created on first use
@@ -101,10 +104,14 @@ inline bool uneven_lengths(const gasalx_params &p, const uint32_t *q_lens, const
     return hi >= lo + 2;
 }
 
-// Host-side check for BatchShape::one_t8: one padded target length in the batch.
-inline bool one_pad8(const uint32_t *t_lens, uint32_t n) {
+// Host-side check for BatchShape::one_t8: one padded target length in the batch, and it is the
+// padded max_t the plan is sized for (a caller's max_t_len is only an upper bound, and a chunk of
+// the host pipeline may hold only shorter targets: the class launch then covers no pair, so the
+// histogram decides)
+inline bool one_pad8(const uint32_t *t_lens, uint32_t n, uint32_t max_t) {
     if (!t_lens || n == 0) return false;
     const uint32_t w = (t_lens[0] + 7) >> 3;
+    if (w != (max_t + 7) >> 3) return false;
     for (uint32_t i = 1; i < n; i++)
         if (((t_lens[i] + 7) >> 3) != w) return false;
     return true;

@@ -624,7 +624,7 @@ void gasal_aln_async(gasal_gpu_storage_t *gs, const uint32_t qbytes, const uint3
     gx::BatchShape shape;
     shape.max_q = mq; shape.max_t = mt;
     shape.sort = gx::uneven_lengths(P, gs->host_query_batch_lens, gs->host_target_batch_lens, n);
-    shape.one_t8 = gx::one_pad8(gs->host_target_batch_lens, n);
+    shape.one_t8 = gx::one_pad8(gs->host_target_batch_lens, n, shape.max_t);
     gx::Workspace *ws = workspace_for(gs);
     // get_tb may run past the batch into the rest of unpacked_query_batch (Q14)
     if (gx::align_device(*ws, P, B, R, st, shape, gs->gpu_max_query_batch_bytes) != GASALX_OK) {

@@ -347,11 +347,74 @@ int gasalx_multi_pairhmm_quals_host(gasalx_multi *m, const gasalx_hmm_qual_batch
     });
 }
 
-// (the calling thread's current device is restored on every exit: a torch caller's
-// current_device must not move to the last entry's device)
 static int multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
                            void *const *streams);
 
+// Device-resident shards: fn(i, stream) queues entry i's work on its stream (one host thread per
+// entry with pairs: a call without max lengths reads them back, which synchronises that stream),
+// then the optional gather of `elem`-byte results (gather_stride per entry), then, with no
+// caller streams, the wait for every entry.
+extern "C++" template <class F>
+static int run_device(gasalx_multi *m, const uint32_t *counts, void *const *streams, const void *const *send,
+                      void *const *gather, uint32_t gather_stride, uint32_t elem, F fn) {
+    const int nd = (int)m->engines.size();
+    std::vector<hipStream_t> st(nd);
+    for (int i = 0; i < nd; i++) st[i] = streams && streams[i] ? (hipStream_t)streams[i] : gx::engine_stream(m->engines[i]);
+    if (gather) {
+        for (int i = 0; i < nd; i++)
+            if (counts[i] > gather_stride || !gather[i] || (counts[i] && !send[i])) {
+                gx::set_error("gather: every entry needs a result buffer of gather_stride >= its pairs and a receive buffer");
+                return GASALX_EINVAL;
+            }
+    }
+    std::vector<uint32_t> bounds(nd + 1);
+    for (int i = 0; i < nd; i++) bounds[i + 1] = bounds[i] + 1;   // one "shard" per entry (run_sharded's form)
+    int rc = run_sharded(m, bounds, [&](int i, uint32_t, uint32_t) -> int {
+        return counts[i] ? fn(i, st[i]) : GASALX_OK;
+    });
+    if (rc) return rc;
+    if (gather) {
+        std::vector<void *> sp(nd);
+        for (int i = 0; i < nd; i++) sp[i] = st[i];
+        rc = multi_allgather(m, send, (void *const *)gather, (uint64_t)gather_stride * elem, sp.data());
+        if (rc) return rc;
+    }
+    if (!streams)
+        for (int i = 0; i < nd; i++) {
+            (void)hipSetDevice(m->devices[i]);
+            const hipError_t e = hipStreamSynchronize(st[i]);
+            if (e != hipSuccess) { gx::set_error(std::string("multi device call: ") + hipGetErrorString(e)); return GASALX_EDEVICE; }
+        }
+    return GASALX_OK;
+}
+
+int gasalx_multi_align_device(gasalx_multi *m, const gasalx_params *params, const gasalx_batch *batches,
+                              const gasalx_results *outs, void *const *streams, int32_t *const *gather,
+                              uint32_t gather_stride) {
+    if (!m || !params || !batches || !outs) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    DeviceGuard guard;
+    const int nd = (int)m->engines.size();
+    std::vector<uint32_t> counts(nd);
+    std::vector<const void *> send(nd);
+    for (int i = 0; i < nd; i++) { counts[i] = batches[i].n_alns; send[i] = outs[i].aln_score; }
+    return run_device(m, counts.data(), streams, send.data(), (void *const *)gather, gather_stride, 4,
+                      [&](int i, hipStream_t st) { return gasalx_align_device(m->engines[i], params, &batches[i], &outs[i], st); });
+}
+
+int gasalx_multi_pairhmm_device(gasalx_multi *m, const gasalx_hmm_batch *batches, float *const *results,
+                                void *const *streams, float *const *gather, uint32_t gather_stride) {
+    if (!m || !batches || !results) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    DeviceGuard guard;
+    const int nd = (int)m->engines.size();
+    std::vector<uint32_t> counts(nd);
+    std::vector<const void *> send(nd);
+    for (int i = 0; i < nd; i++) { counts[i] = batches[i].n_pairs; send[i] = results[i]; }
+    return run_device(m, counts.data(), streams, send.data(), (void *const *)gather, gather_stride, 4,
+                      [&](int i, hipStream_t st) { return gasalx_pairhmm_device(m->engines[i], &batches[i], results[i], st); });
+}
+
+// (the calling thread's current device is restored on every exit: a torch caller's
+// current_device must not move to the last entry's device)
 int gasalx_multi_allgather(gasalx_multi *m, const void *const *send, void *const *recv, uint64_t bytes,
                            void *const *streams) {
     DeviceGuard guard;

@@ -3,9 +3,10 @@
 //
 // The reference finds start positions with a second, reversed DP pass that
 // stops early.  Both reverse passes are the forward kernel of the same
-// algorithm run over materialised reversed sequences; each reversed sequence
-// is "the first L bases of the original, reversed", written into a slot of
-// pad8(max) bytes (so one-to-many offsets need no care), N-filled after L.
+// algorithm reading the forward sequences backwards (WfArgs::rev): each reversed
+// sequence is "the first L bases of the original, reversed", N after L, read in
+// place at the pair's own offsets (round 4 wrote them into slots first: a
+// prep kernel of 0.33 ms per 1 M config-2 pairs).
 //
 // LOCAL (Non-CDP/GASAL2/src/kernels/local_kernel_template.h:441-511).  From the
 // 8-base words holding the end cell (rend_reg = min((q_end>>3)+1, qregs), same
@@ -51,9 +52,10 @@
 //           reverse pass leaves maxXY_x at ref_len, Q10); no last-row cell at
 //           all leaves maxXY_y = 0.
 //
-// Slots are sorted by reversed target words, longest first (counting sort): a
-// wave's step count is set by its longest target, and unrelated pairs end
-// early, so their reversed rectangles are short.
+// The reverse pass's slots are sorted by reversed target words, longest first
+// (counting sort, perm: slot -> pair): a wave's step count is set by its longest
+// target, and unrelated pairs end early, so their reversed rectangles are short.
+// Lengths and results of the reverse pass are per pair.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -61,20 +63,6 @@
 namespace gx {
 
 enum RevMode { REV_LOCAL = 0, REV_SEMI = 1, REV_PLAIN = 2 };   // PLAIN: sort by the lengths given
-
-struct RevArgs {
-    const uint8_t *q, *t;               // input batch (unpacked bytes or packed words)
-    const uint32_t *qoff, *toff, *qlen, *tlen;
-    const int32_t *qend, *tend, *score; // forward results
-    uint8_t *rq, *rt;                   // reversed slots: slot i at i*q8 / i*t8
-    uint32_t *rqoff, *rtoff, *rqlen, *rtlen;
-    int32_t *stop;                      // SEMI: forward score per slot
-    uint32_t n, q8w, t8w;               // words (of 8 bases) per slot
-    int32_t packed, mode;
-    uint32_t fill;                      // 8 pad bytes' value (N_CODE replicated), as two words
-    uint32_t nval;                      // N_CODE & 0xF
-    const uint32_t *perm;               // slot i -> pair perm[i]
-};
 
 __device__ __forceinline__ uint32_t start_regs(uint32_t len, int32_t end) {
     const uint32_t regs = (len + 7) >> 3;
@@ -102,34 +90,6 @@ __device__ __forceinline__ uint32_t seq_byte(const uint8_t *seq, uint32_t off, u
     return (w >> (28 - 4 * (pos & 7))) & 15u;
 }
 
-// word w (8 bytes) of "the first L bases at `off`, reversed", N-filled after L
-__device__ __forceinline__ uint2 rev_first(const uint8_t *seq, uint32_t off, uint32_t L, uint32_t w, int packed,
-                                           uint32_t fill) {
-    if (8 * w >= L) return make_uint2(fill, fill);
-    // output byte j = position L-1-8w-j; positions below 0 are fill
-    const int32_t st = (int32_t)L - 8 - 8 * (int32_t)w;
-    if (!packed) {
-        const int32_t a0 = st >= 0 ? st / 8 : -1, sh = st - 8 * a0;
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(seq + off);
-        const uint64_t lo = a0 >= 0 ? src[a0] : 0ull, hi = sh ? src[a0 + 1] : 0ull;   // within the first L bytes' words
-        uint64_t x = sh ? ((lo >> (8 * sh)) | (hi << (64 - 8 * sh))) : lo;             // bytes st .. st+7
-        x = __builtin_bswap64(x);                                                      // byte j = position st+7-j
-        const uint32_t keep = L - 8 * w;
-        if (keep < 8) {
-            const uint64_t m = (1ull << (8 * keep)) - 1ull;
-            x = (x & m) | ((((uint64_t)fill << 32) | fill) & ~m);
-        }
-        return make_uint2((uint32_t)x, (uint32_t)(x >> 32));
-    }
-    uint32_t b[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int32_t p = st + 7 - j;
-        b[j] = p >= 0 ? seq_byte(seq, off, (uint32_t)p, 1) : (fill & 0xFFu);
-    }
-    return make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24), b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
-}
-
 // sort key of the reverse pass's slots: the reversed target length, or (LOCAL with the forward
 // scores, whose sweep stops once the score is reached) the shorter of it and a span estimate of
 // the alignment, 2 * ceil(score / match) + 16 columns -- a wave's step count is set by its
@@ -145,6 +105,28 @@ __device__ __forceinline__ uint32_t rev_bucket(int32_t mode, const uint32_t *tle
     return t8w - min((L + 7) >> 3, t8w);   // 0 = longest
 }
 
+// cnt[b] += the number of active lanes of the wave with bucket b, one LDS atomic per distinct
+// bucket of the wave (a lane per bucket adds the whole group's count); returns the lane's position
+// among them (the old count + its rank in the group).  The per-lane LDS atomics this replaces
+// serialised on the few buckets of a batch (config 2: ~20 distinct, 48 us per 1 M pairs).
+__device__ __forceinline__ uint32_t wave_bucket_add(uint32_t *cnt, uint32_t b, bool active) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t todo = __ballot(active);
+    uint32_t pos = 0;
+    while (todo) {                                   // wave-uniform: one pass per distinct bucket
+        const int leader = __builtin_ctzll(todo);
+        const uint32_t lb = __shfl(b, leader);
+        const bool mine = active && b == lb;
+        const uint64_t m = __ballot(mine);
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(&cnt[lb], (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        if (mine) pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        todo &= ~m;
+    }
+    return pos;
+}
+
 __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                        uint32_t n, uint32_t t8w, uint32_t *hist,
                                                        const int32_t *score = nullptr, int32_t a = 1) {
@@ -152,7 +134,7 @@ __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint3
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) atomicAdd(&cnt[rev_bucket(mode, tlen, tend, k, t8w, score, a)], 1u);
+    (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a) : 0u, k < n);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
         if (cnt[i]) atomicAdd(&hist[i], cnt[i]);
@@ -184,8 +166,8 @@ __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const ui
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t b = 0, local = 0;
-    if (k < n) { b = rev_bucket(mode, tlen, tend, k, t8w, score, a); local = atomicAdd(&cnt[b], 1u); }
+    const uint32_t b = k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a) : 0u;
+    const uint32_t local = wave_bucket_add(cnt, b, k < n);
     __syncthreads();
     for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
         if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
@@ -196,63 +178,45 @@ __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const ui
     }
 }
 
-// one thread per slot: the reversed lengths (LOCAL: the end words, less the trailing N pads, a
-// loop of dependent byte loads done once per pair) and the slot's offsets
-__global__ __launch_bounds__(256) void rev_len_kernel(RevArgs A) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n) return;
-    const uint32_t k = A.perm[i];
-    const uint32_t ql = A.qlen[k];
+// one thread per pair: the reversed lengths (LOCAL: the end words, less the trailing N pads, a
+// loop of dependent byte loads done once per pair), which the reverse pass reads the forward
+// sequences backwards with (WfArgs::rev)
+__global__ __launch_bounds__(256) void rev_len_kernel(int32_t mode, const uint8_t *q, const uint32_t *qoff,
+                                                      const uint32_t *qlen, const uint32_t *tlen, const int32_t *qend,
+                                                      const int32_t *tend, int32_t packed, uint32_t nval, uint32_t n,
+                                                      uint32_t *rqlen, uint32_t *rtlen) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t ql = qlen[k];
     uint32_t L = ql;
-    if (A.mode == REV_LOCAL) {
-        const uint32_t off = A.qoff[k];
-        L = 8 * start_regs(ql, A.qend[k]);
-        while (L > ql && seq_byte(A.q, off, L - 1, A.packed) % 16u == A.nval) --L;
+    if (mode == REV_LOCAL) {
+        const uint32_t off = qoff[k];
+        L = 8 * start_regs(ql, qend[k]);
+        while (L > ql && seq_byte(q, off, L - 1, packed) % 16u == nval) --L;
     }
-    A.rqoff[i] = i * A.q8w * 8;
-    A.rqlen[i] = L;
-    A.rtoff[i] = i * A.t8w * 8;
-    A.rtlen[i] = rev_tlen(A.mode, A.tlen, A.tend, k);
-    if (A.stop) A.stop[i] = A.score[k];
+    rqlen[k] = L;
+    rtlen[k] = rev_tlen(mode, tlen, tend, k);
 }
 
-// one thread per (slot, 8-base word of the two reversed sequences of the slot's pair), the
-// lengths from rev_len_kernel
-__global__ __launch_bounds__(256) void rev_prep_kernel(RevArgs A) {
-    const uint32_t per = A.q8w + A.t8w;
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (uint64_t)A.n * per) return;
-    const uint32_t i = (uint32_t)(gid / per), w = (uint32_t)(gid - (uint64_t)i * per);
-    const uint32_t k = A.perm[i];
-    if (w < A.q8w)
-        *reinterpret_cast<uint2 *>(A.rq + (uint64_t)i * A.q8w * 8 + 8u * w) =
-            rev_first(A.q, A.qoff[k], A.rqlen[i], w, A.packed, A.fill);
-    else
-        *reinterpret_cast<uint2 *>(A.rt + (uint64_t)i * A.t8w * 8 + 8u * (w - A.q8w)) =
-            rev_first(A.t, A.toff[k], A.rtlen[i], w - A.q8w, A.packed, A.fill);
-}
-
-// one thread per slot i (pair perm[i])
-__global__ __launch_bounds__(256) void start_map_kernel(int32_t mode, const uint32_t *perm, const int32_t *score,
-                                                        const uint32_t *qlen, const uint32_t *rqlen,
-                                                        const uint32_t *tlen, const int32_t *tend,
-                                                        const int32_t *rscore, const int32_t *rqend,
-                                                        const int32_t *rtend, int32_t *qstart, int32_t *tstart,
-                                                        uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = perm[i];
+// one thread per pair k: the reverse pass's ends -> the reference's start fields
+__global__ __launch_bounds__(256) void start_map_kernel(int32_t mode, const int32_t *score, const uint32_t *qlen,
+                                                        const uint32_t *rqlen, const uint32_t *tlen,
+                                                        const int32_t *tend, const int32_t *rscore,
+                                                        const int32_t *rqend, const int32_t *rtend, int32_t *qstart,
+                                                        int32_t *tstart, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
     int32_t qs = 0, ts = 0;
     if (mode == REV_LOCAL) {
         if (score[k] > 0) {   // local_kernel_template.h:468 loop guard maxHH < fwd_score
             const int32_t gr = (int32_t)start_regs(tlen[k], tend[k]);
-            const int32_t r = rqend[i], c = rtend[i];
-            qs = (int32_t)rqlen[i] - 1 - r;                    // ridx counts down (true rows)
+            const int32_t r = rqend[k], c = rtend[k];
+            qs = (int32_t)rqlen[k] - 1 - r;                    // ridx counts down (true rows)
             ts = 8 * gr - 1 - 8 * (c >> 3) + (c & 7);          // gidx + (m-1), Q8
         }
     } else {
         const int32_t tl = (int32_t)tlen[k];
-        const int32_t y = rscore[i] > -32768 ? 8 * semi_gend_reg(tlen[k], tend[k]) + rtend[i] : 0;
+        const int32_t y = rscore[k] > -32768 ? 8 * semi_gend_reg(tlen[k], tend[k]) + rtend[k] : 0;
         ts = tl - 1 - y;                                       // semiglobal :380
         qs = (int32_t)qlen[k] - 1 - tl;                        // :381, maxXY_x = ref_len (Q10)
     }

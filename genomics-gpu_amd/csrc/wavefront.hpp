@@ -69,6 +69,10 @@ struct WfArgs {
     // (j+1)*2^kseg_shift); the keys of every finished segment, [wave][segment < kseg_n][64 lanes][R]
     uint32_t *kseg;
     uint32_t kseg_shift, kseg_n;
+    // WITH_START reverse pass (start.hpp): the sequences are read backwards in place -- qlen / tlen
+    // (per pair) are the reversed lengths L, position p of a reversed sequence is position L-1-p at
+    // the pair's offset, positions p >= L are N (nval)
+    int32_t rev;
 };
 
 constexpr int kWavesPerBlock = 4;
@@ -106,6 +110,42 @@ __device__ __forceinline__ uint32_t load4_codes(const uint8_t *base, uint32_t of
     const uint32_t half = (w & 1) ? (word & 0xFFFFu) : (word >> 16);   // 4 nibbles, first in bits 15:12
     return ((half >> 12) & 15u) | (((half >> 8) & 15u) << 8) | (((half >> 4) & 15u) << 16) |
            ((half & 15u) << 24);
+}
+
+// the same 4 positions of "the first L bases at `off`, reversed" (start.hpp), N (nval) from L on:
+// position p is the original L-1-p, so the 4 bytes are the original [L-4-4w, L-4w) byte-swapped
+// (sequences are padded to 8 bytes: every word read lies inside the pair's padded bytes)
+__device__ __forceinline__ uint32_t load4_codes_rev(const uint8_t *base, uint32_t off, uint32_t L, uint32_t w,
+                                                    int packed, uint32_t nval) {
+    const int32_t st = (int32_t)L - 4 - 4 * (int32_t)w;   // original position of byte 3
+    if (st <= -4) return nval * 0x01010101u;
+    uint32_t x;
+    if (!packed) {
+        const int32_t a = st >> 2, sh = st & 3;              // floor: a >= -1
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(base + off);
+        const uint32_t lo = a >= 0 ? src[a] : 0u, hi = sh ? src[a + 1] : 0u;
+        x = sh ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh) : lo;   // bytes st .. st+3
+        x = __builtin_bswap32(x) & 0x0F0F0F0Fu;             // byte j = position st+3-j
+    } else {
+        x = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int32_t q = st + 3 - j;
+            if (q >= 0) {
+                const uint32_t wd = reinterpret_cast<const uint32_t *>(base)[(off >> 3) + ((uint32_t)q >> 3)];
+                x |= ((wd >> (28 - 4 * (q & 7))) & 15u) << (8 * j);
+            }
+        }
+    }
+    if (st < 0) {                                            // bytes j >= L - 4w are past the sequence
+        const uint32_t keep = L - 4 * w, m = (1u << (8 * keep)) - 1u;
+        x = (x & m) | (nval * 0x01010101u & ~m);
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t load4_codes_dir(const WfArgs &A, const uint8_t *base, uint32_t off, uint32_t L,
+                                                    uint32_t w) {
+    return A.rev ? load4_codes_rev(base, off, L, w, A.packed, (uint32_t)A.nval) : load4_codes(base, off, w, A.packed);
 }
 
 template <int ALGO, bool KEYS, bool TB, int G, int R, bool EXACT, bool STOP>
@@ -351,15 +391,15 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
     }
 }
 
-template <int ALGO, bool KEYS, bool TB, int G, int R, bool STOP = false>
-__global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+// One block's pairs (virtual block bx) of the int32 kernel.
+template <int ALGO, bool KEYS, bool TB, int G, int R, bool STOP>
+__device__ __forceinline__ void wf_block(const WfArgs &A, uint8_t *lds, const uint32_t bx) {
     constexpr int P = 64 / G;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t lg = lane & (G - 1);
     const uint32_t slot = lane / G;
-    const uint32_t pair0 = (blockIdx.x * kWavesPerBlock + wave) * P;
+    const uint32_t pair0 = (bx * kWavesPerBlock + wave) * P;
     const uint32_t idx = pair0 + slot;   // slot; the pair is perm[slot] when sorted
     // pairs the packed kernel already aligned are skipped (dispatch.hip); its flags are per block of slots
     const uint32_t nn = A.n_dev ? min(*A.n_dev, A.n) : A.n;   // (traceback fallback: a device-side count)
@@ -382,9 +422,10 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
         const uint32_t src_lane = ps * G;
         const uint32_t ptp = __shfl(tpad, src_lane);
         const uint32_t pto = __shfl(to, src_lane);
+        const uint32_t ptl = __shfl(tl, src_lane);
         if (idx < P * words) {
             uint32_t v = 0xFFFFFFFFu;
-            if (4u * w < ptp) v = load4_codes(A.t, pto, w, A.packed);
+            if (4u * w < ptp) v = load4_codes_dir(A, A.t, pto, ptl, w);
             reinterpret_cast<uint32_t *>(wlds + ps * stride)[w] = v;
         }
     }
@@ -398,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
 #pragma unroll
     for (int k = 0; k < R; k += 4) {
         uint32_t v = 0xFFFFFFFFu;
-        if (valid && r0 + k < qpad) v = load4_codes(A.q, qo, (r0 + k) >> 2, A.packed);
+        if (valid && r0 + k < qpad) v = load4_codes_dir(A, A.q, qo, ql, (r0 + k) >> 2);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             qc[k + j] = (v >> (8 * j)) & 0xFFu;
@@ -420,6 +461,19 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
         wf_body<ALGO, KEYS, TB, G, R, true, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
     else
         wf_body<ALGO, KEYS, TB, G, R, false, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+}
+
+// As the fallback of a packed launch (A.skip) the grid is capped (dispatch.hip wf_fallback_grid)
+// and each block walks the virtual blocks bx, bx + gridDim.x, ...: a batch the packed kernel took
+// whole then costs a few thousand flag reads instead of a full grid of early exits (25 us per
+// 1 M config-2 pairs).  Each wave stages into its own LDS region, so consecutive virtual blocks
+// need no barrier between them beyond those of the body (block-uniform loop).
+template <int ALGO, bool KEYS, bool TB, int G, int R, bool STOP = false>
+__global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t PPB = kWavesPerBlock * (64 / G);
+    const uint32_t nblk = (A.n + PPB - 1) / PPB;
+    for (uint32_t bx = blockIdx.x; bx < nblk; bx += gridDim.x) wf_block<ALGO, KEYS, TB, G, R, STOP>(A, lds, bx);
 }
 
 }  // namespace gx

@@ -704,10 +704,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
-            const uint32_t ylen = GT ? __shfl(yl[h], ps * G) : 0u;
+            const uint32_t ylen = __shfl(yl[h], ps * G);
             uint32_t v = 0;
             const bool in = (int32_t)y0 >= 0 && y0 < yp;
-            if (in) v = load4_codes(Y, yof, y0 >> 2, A.packed);
+            if (in) v = load4_codes_dir(A, Y, yof, ylen, y0 >> 2);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const uint32_t l = in ? letter_of((v >> (8 * j)) & 15u, A.nval) : 6u;
@@ -735,8 +735,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (valid[h] && r < xpad[h]) {
-                const uint32_t cde = A.packed ? (load4_codes(X, xo[h], r >> 2, 1) >> (8 * (r & 3))) & 15u
-                                              : (uint32_t)X[xo[h] + r] & 15u;
+                // (WITH_START reverse pass: position r of "the first xl bases, reversed", N past xl)
+                const uint32_t pos = A.rev ? xl[h] - 1u - r : r;
+                const uint32_t cde = A.rev && r >= xl[h] ? (uint32_t)A.nval
+                                     : A.packed ? (load4_codes(X, xo[h], pos >> 2, 1) >> (8 * (pos & 3))) & 15u
+                                                : (uint32_t)X[xo[h] + pos] & 15u;
                 const uint32_t l = letter_of(cde, A.nval);
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T
@@ -1081,11 +1084,56 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
             }
         }
         // ---- strip-major first maximum per pair (Q1) ----
+        // e-drift keys (A.kf16; not K2 / KSEG / the round-2 TB kernel): key = KOFS + H*C' + (C'-1-s),
+        // C' = C + G, s = the step (column c = s - lg).  Decoding every row's key took a 32-bit
+        // division per row and half (4 quarter-rate multiplies each, ~6 % of the config-2 kernel);
+        // instead the lane's largest H comes from its largest key (one division per half), and
+        // among the rows holding it the strip-major first cell is a packed minimum of the 16-bit
+        // codes (strip << 8 | k << 3 | col & 7), rows below that H masked to 0xFFFF.  Rows past
+        // the pair's padded query (garbage rows) never hold a larger H than the last real row
+        // above them in the lane, and tie it only in a later row of the same or a later strip.
+        uint64_t bestv[2] = {0, 0};
+        static_assert(R <= 32, "row index of the merge codes: 5 bits");
+        const bool fastkey = !K2 && !LTB && !KSEG && A.kf16 && A.kf16 + (GX_LOCAL_UKEY ? G : 0) <= 2048;   // strip: 8 bits
+        if (fastkey) {
+            const uint32_t C = A.kf16 + (GX_LOCAL_UKEY ? G : 0);
+            constexpr uint32_t KOFS_ = KU16 ? 0u : 0x0400u;
+            uint32_t km = key[0];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint64_t best = 0;
+            for (int k = 1; k < R; ++k) km = pk_max_u16(km, key[k]);
+            uint32_t thr = 0, Hm[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                Hm[h] = (((km >> (16 * h)) & 0xFFFFu) - KOFS_) / C;
+                thr |= (KOFS_ + Hm[h] * C) << (16 * h);
+            }
+            const uint32_t cb = pk_bcast((int32_t)(C - 1u - (GX_LOCAL_UKEY ? lg : 0u)));   // col = cb - (key - thr)
+            const pk_u2 one = {1, 1}, ffff = {0xFFFF, 0xFFFF};
+            uint32_t bc = 0xFFFFFFFFu;
 #pragma unroll
             for (int k = 0; k < R; ++k) {
+                const uint32_t t = GX_AS(uint32_t, GX_AS(pk_u2, key[k]) - GX_AS(pk_u2, thr));
+                const pk_u2 below = __builtin_elementwise_min(__builtin_elementwise_sub_sat(GX_AS(pk_u2, thr),
+                                                                                            GX_AS(pk_u2, key[k])), one);
+                const uint32_t col = GX_AS(uint32_t, GX_AS(pk_u2, cb) - GX_AS(pk_u2, t));
+                const uint32_t code = (((col & 0xFFF8FFF8u) << 5) | (col & 0x00070007u) | ((uint32_t)(k << 3) * 0x10001u)) |
+                                      GX_AS(uint32_t, below * ffff);
+                bc = GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, bc), GX_AS(pk_u2, code)));
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t c16 = (bc >> (16 * h)) & 0xFFFFu, k = (c16 >> 3) & 31u, r = r0 + k;
+                if (Hm[h] > 0 && c16 != 0xFFFFu && r < xpad[h]) {
+                    const uint32_t ord = (((c16 >> 8) * xpad[h] + r) << 3) + (c16 & 7u);
+                    bestv[h] = ((uint64_t)Hm[h] << 32) | (0xFFFFFFFFu - ord);
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint64_t best = bestv[h];
+#pragma unroll
+            for (int k = 0; k < R && !fastkey; ++k) {
                 const uint32_t r = r0 + k;
                 const uint32_t kk = (key[k] >> (16 * h)) & 0xFFFFu;
                 uint32_t H = kk >> 8, col = 255u - (kk & 0xFFu);
@@ -1103,10 +1151,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     const uint32_t *src = A.kseg + ((size_t)wv * A.kseg_n * 64 + lane) * R + k;
                     for (uint32_t j = 0; j < jseg; ++j) seg(j, src[(size_t)j * (64 * R)]);
                     seg(jseg, key[k]);
-                } else if (!K2 && !LTB && A.kf16) {   // 0x0400 + H*C + (C-1-c) (u16 keys: no 0x0400)
-                    const uint32_t C = A.kf16 + (GX_LOCAL_UKEY ? G : 0), x = kk - (KU16 ? 0u : 0x0400u);
-                    H = x / C;
-                    col = C - 1u - (x - H * C) - (GX_LOCAL_UKEY ? lg : 0u);   // (the step's rank, GX_LOCAL_UKEY)
                 }
                 if constexpr (K2) {   // columns 256..511: later, so they win only when strictly higher
                     const uint32_t k2v = (key2[k] >> (16 * h)) & 0xFFFFu;

@@ -36,7 +36,8 @@ EXPORTS = (
     "gasalx_nv_banded_score_device", "gasalx_nv_banded_score_host",
     "gasalx_multi_create", "gasalx_multi_destroy", "gasalx_multi_info", "gasalx_multi_engine",
     "gasalx_shard_bounds", "gasalx_multi_align_host", "gasalx_multi_pairhmm_host",
-    "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather",
+    "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather", "gasalx_packed_pairs",
+    "gasalx_multi_align_device", "gasalx_multi_pairhmm_device",
 )
 MULTI_RCCL = 1
 
@@ -286,10 +287,11 @@ class Engine:
             pass
 
     def align_host(self, batch: Batch, params: Params, q_ops=None, t_ops=None, seed_scores=None, fields=None,
-                   cigar_out=None):
+                   cigar_out=None, max_q_len=0, max_t_len=0):
         """fields: the result arrays to request (default all; the rest are passed as NULL).
         cigar_out: optional caller-owned uint8 array of q_bytes for the CIGAR buffer (e.g. a
-        page-locked one, as the reference's own host_res, res.cpp:8-70), used as given."""
+        page-locked one, as the reference's own host_res, res.cpp:8-70), used as given.
+        max_q_len / max_t_len: the batch's upper bounds of the lengths (gasalx.h; 0 = from the lengths)."""
         n = batch.n
         out = {k: np.full(n, SENTINEL, np.int32) for k in (OUT_FIELDS if fields is None else fields)}
         tb = params.start_pos == WITH_TB          # CIGAR buffers only when the reference fills them
@@ -305,7 +307,7 @@ class Engine:
         to = None if t_ops is None else np.ascontiguousarray(t_ops, np.uint8)
         sd = None if seed_scores is None else np.ascontiguousarray(seed_scores, np.uint32)
         cb = CBatch(_p(batch.q_data), _p(batch.q_offsets), _p(batch.q_lens), _p(batch.t_data), _p(batch.t_offsets),
-                    _p(batch.t_lens), batch.q_bytes, batch.t_bytes, n, _p(qo), _p(to), _p(sd), 0, 0)
+                    _p(batch.t_lens), batch.q_bytes, batch.t_bytes, n, _p(qo), _p(to), _p(sd), max_q_len, max_t_len)
         cr = CResults(*(_p(out[k]) if k in out else None for k in OUT_FIELDS), _p(cigar) if tb else None,
                       _p(n_ops) if tb else None)
         _check(lib().gasalx_align_host(self._h, ctypes.byref(params), ctypes.byref(cb), ctypes.byref(cr)),
@@ -313,6 +315,13 @@ class Engine:
         out["cigar"] = cigar
         out["n_ops"] = n_ops
         return out
+
+    def packed_pairs(self):
+        """(handled, total): pairs of the last packed launches the packed kernels aligned themselves
+        (gasalx_packed_pairs); the rest went to the int32 kernel."""
+        h, t = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib().gasalx_packed_pairs(self._h, ctypes.byref(h), ctypes.byref(t)), "packed_pairs")
+        return int(h.value), int(t.value)
 
     def align_device_ptrs(self, params: Params, ptrs: dict, q_bytes: int, t_bytes: int, n: int, max_q: int,
                           max_t: int, stream: int = 0):
@@ -477,6 +486,45 @@ class Multi:
         hb = hmm.cstruct()
         _check(lib().gasalx_multi_pairhmm_quals_host(self._h, ctypes.byref(hb), _p(res)), "multi_pairhmm_quals_host")
         return res
+
+    def align_device_ptrs(self, params: "Params", shards, streams=None, gather=None, gather_stride: int = 0):
+        """Device-resident shards (gasalx_multi_align_device): shards[i] is a dict as
+        Engine.align_device_ptrs takes (integer device addresses on entry i's device) plus "q_bytes",
+        "t_bytes", "n", "max_q", "max_t"; gather: one receive address per entry (world x
+        gather_stride int32) or None."""
+        k = len(self.devices)
+        if len(shards) != k:
+            raise ValueError("one shard per device entry")
+        g = lambda d, key: d.get(key) or None
+        cbs = (CBatch * k)(*[CBatch(g(d, "q_batch"), g(d, "q_offsets"), g(d, "q_lens"), g(d, "t_batch"),
+                                    g(d, "t_offsets"), g(d, "t_lens"), d["q_bytes"], d["t_bytes"], d["n"],
+                                    g(d, "q_ops"), g(d, "t_ops"), g(d, "seed_scores"), d.get("max_q", 0),
+                                    d.get("max_t", 0)) for d in shards])
+        crs = (CResults * k)(*[CResults(g(d, "aln_score"), g(d, "q_end"), g(d, "t_end"), g(d, "q_start"),
+                                        g(d, "t_start"), g(d, "aln_score2"), g(d, "q_end2"), g(d, "t_end2"),
+                                        g(d, "cigar"), g(d, "n_cigar_ops")) for d in shards])
+        sts = None if streams is None else (ctypes.c_void_p * k)(*streams)
+        gat = None if gather is None else (ctypes.c_void_p * k)(*gather)
+        _check(lib().gasalx_multi_align_device(self._h, ctypes.byref(params), cbs, crs, sts, gat,
+                                               ctypes.c_uint32(gather_stride)), "multi_align_device")
+
+    def pairhmm_device_ptrs(self, shards, streams=None, gather=None, gather_stride: int = 0):
+        """Device-resident PairHMM shards (gasalx_multi_pairhmm_device): shards[i] holds the device
+        addresses of Engine.pairhmm_device_ptrs's arrays plus "result", "read_bytes", "hap_bytes",
+        "n", "max_r", "max_h"."""
+        k = len(self.devices)
+        if len(shards) != k:
+            raise ValueError("one shard per device entry")
+        g = lambda d, key: d.get(key) or None
+        hbs = (CHmmBatch * k)(*[CHmmBatch(g(d, "reads"), g(d, "read_offsets"), g(d, "read_lens"), g(d, "qm"),
+                                          g(d, "delta"), g(d, "xiksi"), g(d, "alpha"), g(d, "haps"),
+                                          g(d, "hap_offsets"), g(d, "hap_lens"), d["read_bytes"], d["hap_bytes"],
+                                          d["n"], d.get("max_r", 0), d.get("max_h", 0)) for d in shards])
+        res = (ctypes.c_void_p * k)(*[d["result"] for d in shards])
+        sts = None if streams is None else (ctypes.c_void_p * k)(*streams)
+        gat = None if gather is None else (ctypes.c_void_p * k)(*gather)
+        _check(lib().gasalx_multi_pairhmm_device(self._h, hbs, res, sts, gat, ctypes.c_uint32(gather_stride)),
+               "multi_pairhmm_device")
 
     def allgather_ptrs(self, send_ptrs, recv_ptrs, nbytes: int, streams=None):
         """Device buffers (integer addresses), one send and one recv per entry."""

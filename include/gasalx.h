@@ -129,6 +129,13 @@ int gasalx_host_free(void *ptr);
 int gasalx_describe_plan(const gasalx_params *params, uint32_t max_q_len, uint32_t max_t_len, char *buf,
                          uint32_t buf_len);
 
+/* Diagnostics: pairs of the engine's last packed (two-pairs-per-lane) launches that the packed
+ * kernel aligned itself (*handled) out of the pairs those launches covered (*total); the rest went
+ * to the int32 kernel.  The engine's own workspace and its two host-pipeline stages each count
+ * their last packed launch (a WITH_START call: the reverse pass) and forgets it once read.
+ * Synchronises the engine's streams; 0 / 0 when no packed launch ran since the last read. */
+int gasalx_packed_pairs(gasalx_engine *engine, uint64_t *handled, uint64_t *total);
+
 /* PairHMM forward.  Per read base: read byte and the four per-base parameters
  * (qm = ph2pr[bq], delta = ph2pr[iq], xiksi = ph2pr[dq], alpha = 1 - ph2pr[(iq+dq)&127],
  * tile_1.cu:415-419) at the read's offset; haplotype bytes at hap offsets. */
@@ -304,6 +311,21 @@ int gasalx_multi_align_host(gasalx_multi *m, const gasalx_params *params, const 
                             const gasalx_results *host_out);
 int gasalx_multi_pairhmm_host(gasalx_multi *m, const gasalx_hmm_batch *host_batch, float *host_result);
 int gasalx_multi_pairhmm_quals_host(gasalx_multi *m, const gasalx_hmm_qual_batch *host_batch, float *host_result);
+/* Device-resident shards (a batch already split over the entries' devices, as config 4's
+ * 10 M reads would sit in HBM): entry i aligns batches[i] -- device arrays on its own device,
+ * max_q_len / max_t_len set, or the lengths are read back -- into outs[i] on streams[i] (NULL:
+ * the entry's engine stream), one host thread per entry.  gather (optional, NULL to skip): the
+ * exchange step in the same call, every entry's aln_score (padded to gather_stride int32 per
+ * entry: each aln_score buffer holds gather_stride entries) lands at gather[j] + i * gather_stride
+ * on every entry j (gasalx_multi_allgather: RCCL when the group has a communicator, else peer
+ * copies).  With streams given the call returns once the work is queued; with NULL it waits. */
+int gasalx_multi_align_device(gasalx_multi *m, const gasalx_params *params, const gasalx_batch *batches,
+                              const gasalx_results *outs, void *const *streams, int32_t *const *gather,
+                              uint32_t gather_stride);
+/* The same for PairHMM: entry i scores batches[i] into results[i] (float, gather_stride entries
+ * when gathering), then the optional gather of the float results. */
+int gasalx_multi_pairhmm_device(gasalx_multi *m, const gasalx_hmm_batch *batches, float *const *results,
+                                void *const *streams, float *const *gather, uint32_t gather_stride);
 /* The exchange step: entry i's `bytes` at send[i] (device memory of its device) land at
  * recv[j] + i * bytes on every entry j.  streams: one hipStream_t per entry (the call
  * is then asynchronous), or NULL for the engines' streams and a synchronous call. */

@@ -170,21 +170,115 @@ def test_multi_distinct_devices_align_and_gather():
     assert _gather_case(devs, rccl=True) is True
 
 
-@pytest.mark.parametrize("workload,pairs,checked", [("semi", 200_000, 200_000), ("nw_tb", 20_000, 40_000)])
-def test_bench_two_ranks_gloo_one_gpu(workload, pairs, checked):
-    # the exact N = 2 bench path on one device: torch.distributed.run spawns 2 ranks, each
+def _device_entries():
+    # the box's distinct devices when it has several (at most 4), else entry 0 twice
+    n = _device_count()
+    return list(range(min(n, 4))) if n >= 2 else [0, 0]
+
+
+def test_multi_align_device_resident_shards_and_gather():
+    # gasalx_multi_align_device: each entry's shard already in its device's
+    # memory, one stream per entry, then the score gather in the same call; every shard's outputs
+    # and every entry's gathered scores against the oracle
+    import torch
+    devs = _device_entries()
+    k = len(devs)
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.TARGET)
+    b = G.Batch.synth(4, 50_001, 0x5EED0004)
+    o = O.align(b, O.make_params(**kw))
+    bounds = G.shard_bounds(b.q_lens, b.t_lens, k)
+    stride = max(e - s for s, e in bounds)
+    m = G.Multi(devs, rccl=True)
+    keep, shards, gat, streams = [], [], [], []
+    for (s, e), d in zip(bounds, devs):
+        sb = b.slice(s, e)
+        dev = f"cuda:{d}"
+        t = {"q_batch": torch.from_numpy(sb.q_data).to(dev), "t_batch": torch.from_numpy(sb.t_data).to(dev)}
+        for f in ("q_offsets", "t_offsets", "q_lens", "t_lens"):
+            t[f] = torch.from_numpy(getattr(sb, f).view(np.int32).copy()).to(dev)
+        t["aln_score"] = torch.full((stride,), -7, dtype=torch.int32, device=dev)
+        t["q_end"] = torch.empty(e - s, dtype=torch.int32, device=dev)
+        t["t_end"] = torch.empty(e - s, dtype=torch.int32, device=dev)
+        g = torch.full((k * stride,), -1, dtype=torch.int32, device=dev)
+        st = torch.cuda.Stream(dev)
+        keep.append((t, g, st))
+        shard = {f: v.data_ptr() for f, v in t.items()}
+        shard.update(q_bytes=sb.q_bytes, t_bytes=sb.t_bytes, n=e - s, max_q=int(sb.q_lens.max()),
+                     max_t=int(sb.t_lens.max()))
+        shards.append(shard)
+        gat.append(g.data_ptr())
+        streams.append(st.cuda_stream)
+    torch.cuda.synchronize()
+    m.align_device_ptrs(G.make_params(**kw), shards, gather=gat, gather_stride=stride)   # synchronous
+    m.align_device_ptrs(G.make_params(**kw), shards, streams=streams, gather=gat, gather_stride=stride)
+    for st in streams:
+        torch.cuda.ExternalStream(st).synchronize()
+    want = np.full(k * stride, -7, np.int32)
+    for i, (s, e) in enumerate(bounds):
+        t = keep[i][0]
+        for f, name in (("score", "aln_score"), ("q_end", "q_end"), ("t_end", "t_end")):
+            assert np.array_equal(t[name][:e - s].cpu().numpy(), o[f][s:e]), (i, f)
+        want[i * stride:i * stride + (e - s)] = o["score"][s:e]
+    for i in range(k):
+        assert np.array_equal(keep[i][1].cpu().numpy(), want), f"gather at entry {i}"
+    m.close()
+
+
+def test_multi_pairhmm_device_resident_shards_and_gather():
+    import torch
+    devs = _device_entries()
+    k = len(devs)
+    d = G.HmmData.from_pairs(_hmm_pairs(np.random.default_rng(78), 700))
+    qm, de, xi, al = d.float_params()
+    ref = O.pairhmm(d.reads, d.read_offsets, d.read_lens, qm, de, xi, al, d.haps, d.hap_offsets, d.hap_lens)
+    bounds = G.shard_bounds(d.read_lens, d.hap_lens, k)
+    stride = max(e - s for s, e in bounds)
+    m = G.Multi(devs)
+    keep, shards, gat = [], [], []
+    for (s, e), dv in zip(bounds, devs):
+        dev = f"cuda:{dv}"
+        r0, r1 = int(d.read_offsets[s]), int(d.read_offsets[e - 1] + d.read_lens[e - 1])
+        h0, h1 = int(d.hap_offsets[s]), int(d.hap_offsets[e - 1] + d.hap_lens[e - 1])
+        u = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        t = {"reads": u(d.reads[r0:r1]), "haps": u(d.haps[h0:h1]),
+             "read_offsets": u((d.read_offsets[s:e] - r0).astype(np.int32)), "read_lens": u(d.read_lens[s:e].view(np.int32)),
+             "hap_offsets": u((d.hap_offsets[s:e] - h0).astype(np.int32)), "hap_lens": u(d.hap_lens[s:e].view(np.int32)),
+             "qm": u(qm[r0:r1]), "delta": u(de[r0:r1]), "xiksi": u(xi[r0:r1]), "alpha": u(al[r0:r1]),
+             "result": torch.full((stride,), -1.0, dtype=torch.float32, device=dev)}
+        g = torch.full((k * stride,), -2.0, dtype=torch.float32, device=dev)
+        keep.append((t, g))
+        shard = {f: v.data_ptr() for f, v in t.items()}
+        shard.update(read_bytes=r1 - r0, hap_bytes=h1 - h0, n=e - s)
+        shards.append(shard)
+        gat.append(g.data_ptr())
+    torch.cuda.synchronize()
+    m.pairhmm_device_ptrs(shards, gather=gat, gather_stride=stride)
+    for i, (s, e) in enumerate(bounds):
+        np.testing.assert_allclose(keep[i][0]["result"][:e - s].cpu().numpy(), ref[s:e], rtol=1e-5)
+    g0 = keep[0][1].cpu().numpy()
+    for i in range(k):
+        assert np.array_equal(keep[i][1].cpu().numpy().view(np.uint32), g0.view(np.uint32)), f"gather at entry {i}"
+        s, e = bounds[i]
+        np.testing.assert_allclose(g0[i * stride:i * stride + e - s], ref[s:e], rtol=1e-5)
+    m.close()
+
+
+@pytest.mark.parametrize("workload,pairs,checked,world", [("semi", 200_000, 200_000, 2), ("nw_tb", 20_000, 40_000, 2),
+                                                          ("pairhmm", 8_000, 16_000, 2), ("semi", 200_000, 200_000, 4)])
+def test_bench_ranks_gloo_one_gpu(workload, pairs, checked, world):
+    # the exact N-rank bench path on one device: torch.distributed.run spawns the ranks, each
     # aligns its cell-balanced shard into ScoreGather.buf, the gloo exchange runs in every
-    # timed step, and rank 0 checks the gathered scores of both ranks against the oracle.
-    # nw_tb runs two engines on two streams per rank (its default), each with its own
-    # exchange buffers
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+    # timed step, and rank 0 checks the gathered scores of every rank against the oracle.
+    # nw_tb runs several engines on their own streams per rank (its default), each with its own
+    # exchange buffers; pairhmm gathers fp32 results (config 5, "1 -> 8 GPUs"); semi at world 4
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
            "--workload", workload, "--pairs", str(pairs), "--steps", "3", "--warmup", "1", "--no-e2e"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0 and lines, p.stdout[-2000:] + p.stderr[-4000:]
     out = json.loads(lines[-1])
-    assert out["n_gpus"] == 2 and out["config"]["dist_backend"] == "gloo"
+    assert out["n_gpus"] == world and out["config"]["dist_backend"] == "gloo"
     par = out["parity"]
     assert par["mismatches"] == 0 and par["pairs_checked"] == checked      # nw_tb: pairs per rank (weak)
     assert par["gathered_mismatches"] == 0 and par["gathered_scores_checked"] == checked

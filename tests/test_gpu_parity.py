@@ -139,7 +139,12 @@ def test_local_with_start_wavefront(engine, qr, tr, alphabet, scores):
 
 
 def test_local_with_start_config2_sample(engine):
+    engine.packed_pairs()                                    # forget earlier launches
     check(engine, G.Batch.synth(2, 20000, 0x5EED0002), algo=G.LOCAL, start_pos=G.WITH_START)
+    # the reverse pass (the last packed launch) read the forward sequences backwards on the
+    # packed kernel for every pair (start.hpp, WfArgs::rev)
+    handled, total = engine.packed_pairs()
+    assert total == 20000 and handled == total, (handled, total)
 
 
 def test_local_with_start_shared_query_and_zero_scores(engine):
@@ -1157,6 +1162,46 @@ def test_semiglobal_tail_query_config4(engine, head, tail):
     b = G.Batch.synth(4, 3000, 0x5EED0400 + 4 * head + tail)
     for a, bb, o, e in SEMI_SCORES:
         check(engine, b, algo=G.SEMI_GLOBAL, head=head, tail=tail, match=a, mismatch=bb, gap_open=o, gap_extend=e)
+
+
+@pytest.mark.parametrize("tail", TQ_TAILS)
+def test_semiglobal_tail_query_loose_max_t(engine, tail):
+    # one padded target length in the batch, but a caller's max_t_len (an upper
+    # bound, gasalx.h) above it -- the class launch must be the batch's class, not pad8(max_t)'s,
+    # or every pair falls to the int32 kernel; results equal either way, so the packed count is
+    # what this checks
+    b = G.Batch.synth(4, 6000, 0x5EED0411 + tail)          # 182 bp windows: one class, R = 23
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=tail)
+    o = O.align(b, O.make_params(**kw))
+    for mt in (0, 184, 200, 256):
+        engine.packed_pairs()                                # forget earlier launches
+        g = engine.align_host(b, G.make_params(**kw), max_t_len=mt)
+        for f in ("score", "q_end", "t_end"):
+            assert np.array_equal(g[f], o[f]), (mt, f)
+        handled, total = engine.packed_pairs()
+        assert total >= b.n and handled == total, (mt, handled, total)
+
+
+def test_semiglobal_tail_query_pipeline_chunks_of_shorter_targets(engine):
+    # the host pipeline's chunks (16,384 pairs and up): chunks 1 and 2 hold only 100 bp
+    # targets while the batch's max_t is 182 (capi.cpp per-chunk class check)
+    rng = np.random.default_rng(0x0E7A)
+    n = 3 * 16384
+    qs, ts = [], []
+    for i in range(n):
+        tl = 182 if i < 16384 else 100
+        t = helpers.random_seq(rng, tl)
+        ts.append(t)
+        qs.append(helpers.mutate(rng, t)[: (150 if tl == 182 else 90)])
+    b = G.Batch.from_pairs(qs, ts)
+    kw = dict(algo=G.SEMI_GLOBAL, head=G.TARGET, tail=G.QUERY)
+    engine.packed_pairs()                                    # forget earlier launches
+    g = engine.align_host(b, G.make_params(**kw))
+    o = O.align(b, O.make_params(**kw))
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(g[f], o[f]), f
+    handled, total = engine.packed_pairs()
+    assert total > 0 and handled == total, (handled, total)
 
 
 @pytest.mark.parametrize("tail", TQ_TAILS)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """VALU instruction mix of one kernel's steady loop, from the built library (gfx950 ISA).
 
-usage: kernel_census.py LIB.so|OBJ.co KERNEL_SYMBOL [RATES.json]
+usage: kernel_census.py LIB.so|OBJ.co KERNEL_SYMBOL|"demangled name" [RATES.json]
 
 Extracts the gfx950 code object from the library's fat binary, disassembles the kernel,
 finds its loops (backward branches) and takes the one with the most VALU instructions as
@@ -71,6 +71,19 @@ def price(op, text, table):
     return 4.0
 
 
+def mangled(lib, name):
+    """The code object's kernel symbol whose demangled form is `name` (as rocprofv3 prints it)."""
+    with tempfile.TemporaryDirectory() as tmp:
+        co = lib if lib.endswith(".co") else code_object(lib, tmp)
+        out = subprocess.run([f"{LLVM}/llvm-objdump", "-t", co], check=True, capture_output=True, text=True).stdout
+    syms = sorted({ln.split()[-1] for ln in out.splitlines() if " F " in ln and ln.split()[-1].startswith("_Z")})
+    dem = subprocess.run(["c++filt"], input="\n".join(syms), check=True, capture_output=True, text=True).stdout.split("\n")
+    for m, d in zip(syms, dem):
+        if d.strip() == name.strip():
+            return m
+    raise SystemExit(f"no kernel symbol demangles to {name!r}")
+
+
 def census(lib, sym, rates):
     table = rates_table(rates)
     with tempfile.TemporaryDirectory() as tmp:
@@ -93,10 +106,20 @@ def census(lib, sym, rates):
 
     def arith(seg):
         return sum(1 for _, x, _ in seg if x.startswith(("v_pk_", "v_fma", "v_fmac", "v_mul_f32", "v_perm")))
-    # densest in packed / fp32 arithmetic (the cell updates), among the DPP loops when there are any
-    with_dpp = [g for g in loops if dpp(g) and arith(g) > 0]
-    pool = with_dpp if with_dpp else [g for g in loops if arith(g) > 0] or loops
-    seg = max(pool, key=lambda g: (arith(g) / len(g), -len(g)))
+    # innermost loops (no backward branch inside) carrying the DPP lane hand-offs (wavefront sweeps);
+    # of them the densest in cell arithmetic per VALU instruction: the same sweep with capture or
+    # boundary code, or a sweep the launch's plan does not take (the round-2 LOCAL sweep beside the
+    # e-drift one in the same kernel: 446 against 345 VALU at G8R19), is less dense.  Without DPP
+    # loops (band pass, thread-per-pair kernels): the densest innermost loop.
+    def inner(seg):
+        lo, hi = seg[0][0], seg[-1][0]
+        return not any(t.startswith(("s_cbranch", "s_branch")) and o is not None and lo <= ins[0][0] + o < a
+                       for a, t, o in seg[:-1])
+    nvalu = lambda g: max(1, sum(1 for _, x, _ in g if x.startswith("v_")))
+    innermost = [g for g in loops if inner(g)] or loops
+    with_dpp = [g for g in innermost if dpp(g) and arith(g) > 0]
+    pool = with_dpp or [g for g in innermost if arith(g) > 0] or innermost
+    seg = max(pool, key=lambda g: (arith(g) / nvalu(g), -len(g)))
     best = (0, seg)
     # static census: conditionally executed blocks (divergent captures, resets) are counted
     # too, although the hardware skips them while no lane enters (s_cbranch_execz); the
@@ -115,6 +138,9 @@ def census(lib, sym, rates):
             "rates": os.path.relpath(rates, ROOT)}
 
 
+RATES = os.path.join(ROOT, "profiles", "r04_valu_issue_rates.json")
+
 if __name__ == "__main__":
-    rates = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "r04_valu_issue_rates.json")
-    print(json.dumps(census(sys.argv[1], sys.argv[2], rates), indent=1))
+    rates = sys.argv[3] if len(sys.argv) > 3 else RATES
+    sym = sys.argv[2] if sys.argv[2].startswith("_Z") else mangled(sys.argv[1], sys.argv[2])
+    print(json.dumps(census(sys.argv[1], sym, rates), indent=1))

@@ -61,6 +61,19 @@ def main(run_dir, workload, pairs):
         out["hbm_bytes_per_launch"] = 2 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024
     if "SQ_INSTS_VALU" in c:
         out["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    # the steady loop's instruction mix priced by the measured issue table (kernel_census.py), of the
+    # same library the passes ran (bench.py: the per-class issue-bound fraction)
+    lib = os.path.join(ROOT, "genomics-gpu_amd", "lib", "libgasal.so")
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import hashlib
+        import kernel_census as KC
+        if hashlib.sha256(open(lib, "rb").read()).hexdigest() == out.get("lib_sha256"):
+            c = KC.census(lib, KC.mangled(lib, best), KC.RATES)
+            out["census"] = {k: c[k] for k in ("kernel", "loop_valu", "loop_salu", "loop_issue_cycles",
+                                               "cycles_per_valu", "rates")}
+    except (Exception, SystemExit) as e:   # noqa: BLE001 -- the census is an addition, never a failure
+        out["census_error"] = str(e)
     out["note"] = ("separate rocprofv3 --pmc passes (scripts/pmc_session.sh); FETCH_SIZE x2 per the gfx950 "
                    "correction; counters of the longest dispatch of the dominant kernel")
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
