@@ -53,9 +53,6 @@ namespace gx {
 #ifndef GX_BAND16_WAVES
 #define GX_BAND16_WAVES 3   // waves per SIMD (a few spills; 3.3 % faster than 2 waves at 184 VGPRs)
 #endif
-#ifndef GX_BAND16_SCHED
-#define GX_BAND16_SCHED 0
-#endif
 
 struct BandArgs {
     const uint32_t *qw, *tw;           // packed 4-bit words of the batch
@@ -245,17 +242,11 @@ __global__ __launch_bounds__(256, GX_BAND16_WAVES) void band16_kernel(BandArgs A
                 if (doA) {
                     band_row(TA0, TA1, sel, hoeA, fA, holA, left, e, key, KC, BB, OE2, EXT, C);
                     band_row_max(bA, key, rr);
-#if GX_BAND16_SCHED
-                    __builtin_amdgcn_sched_barrier(0);   // keep strip i and i + 1 rows apart: registers
-#endif
                 }
                 if (doB) {
                     band_row(TB0, TB1, sel, hoeB, fB, holB, left, e, key, KC, BB, OE2, EXT, C);
                     band_row_max(bB, key, rr);
                     rows[((uint32_t)j * 8 + k) * rs] = make_uint2(left, e);
-#if GX_BAND16_SCHED
-                    __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
             }
 #pragma unroll

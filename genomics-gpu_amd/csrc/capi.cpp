@@ -331,18 +331,15 @@ int gasalx_align_host(gasalx_engine *eng, const gasalx_params *params, const gas
     // TB: the traceback walk is latency-bound per chunk whatever its size, so chunks
     // of ~5.5 G padded cells, 2 to 8 of them (1 M x 150 bp: 4, 34.0 ms pageable against
     // 50.5 with 2; 100 K x 300 bp: 2); score-only: 8
-    static const char *chunks_env = std::getenv("GASALX_HOST_CHUNKS");        // A/B knob: chunks per batch
     uint32_t n_chunks = 8;
     if (params->start_pos == 2) {
         const double mq = hb->max_q_len ? hb->max_q_len : host_max(hb->q_lens, n);
         const double mt = hb->max_t_len ? hb->max_t_len : host_max(hb->t_lens, n);
         n_chunks = (uint32_t)std::min(8.0, std::max(2.0, std::round((double)n * mq * mt / 5.5e9)));
     }
-    if (chunks_env) n_chunks = (uint32_t)std::max(1, std::atoi(chunks_env));
     const uint32_t chunk = std::max<uint32_t>(16384, (uint32_t)(((uint64_t)n + n_chunks - 1) / n_chunks));
-    static const bool single = std::getenv("GASALX_HOST_SINGLE") != nullptr;   // A/B knob
     const bool tb = params->start_pos == 2;
-    if (!single && n >= 2 * chunk && !(params->is_packed && tb) && contiguous(hb->q_offsets, hb->q_lens, n, hb->q_bytes) &&
+    if (n >= 2 * chunk && !(params->is_packed && tb) && contiguous(hb->q_offsets, hb->q_lens, n, hb->q_bytes) &&
         contiguous(hb->t_offsets, hb->t_lens, n, hb->t_bytes))
         return align_host_pipelined(eng, params, hb, ho, chunk);
     gasalx_batch db = *hb;

@@ -39,11 +39,6 @@ void DevBuf::release() {
     bytes = 0;
 }
 void Workspace::release_all() {
-    if (walk_stream) { (void)hipStreamSynchronize(walk_stream); (void)hipStreamDestroy(walk_stream); walk_stream = nullptr; }
-    for (Workspace *w : sides) { w->release_all(); delete w; }
-    sides.clear();
-    for (hipEvent_t *x : {&fork, &join, &dp_done})
-        if (*x) { (void)hipEventDestroy(*x); *x = nullptr; }
     for (DevBuf *b : {&packed_q, &packed_t, &tb, &rows_h, &rows_e, &rev, &ends_q, &ends_t, &misc, &aux,
                       &rev_meta, &sort_meta, &band_cp, &band_stm, &band_fl, &band_fb, &kseg}) b->release();
 }
@@ -351,12 +346,9 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             // instruction per two cells) up to 65536 -- either covers targets past 256 columns
             // without the second key set; values B + H + e(r + c) over the shape's span stay in
             // the window and the top lane's first diagonal B - 2e above 0x0400.  GASALX_KF16=0
-            // keeps the round-2 kernel, GASALX_KU16=0 the int32 kernel where only u16 keys fit
-            // (A/B runs)
-            // LOCAL + traceback takes the e-drift kernel with f16 keys (WF16_LOCAL_TBD) when they fit;
-            // GASALX_LTBD=0 keeps the round-2 traceback kernel (A/B)
-            if (wf_algo == WF_LOCAL && env_flag("GASALX_KF16", true) &&
-                (!pl.tb || (GX_LOCAL_UKEY && env_flag("GASALX_LTBD", true)))) {
+            // keeps the round-2 kernel (the tests' cross-check of both key forms)
+            // LOCAL + traceback takes the e-drift kernel with f16 keys (WF16_LOCAL_TBD) when they fit
+            if (wf_algo == WF_LOCAL && env_flag("GASALX_KF16", true)) {
                 const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
                 const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
                 const int64_t hmax = a * std::min(q8, t8), base = 0x400 + oe + k + 16;
@@ -369,8 +361,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 uint32_t mseg = 0;
                 while ((hmax + 1) * (int64_t)(2u << mseg) <= 0x7800 && mseg < 12) ++mseg;   // M = 2^mseg
                 const bool seg_ok = frame && kseg_mode > 0 && mseg >= 2 && y8 <= 0xFFFF;
-                // key range: steps C + G (GX_LOCAL_UKEY, wavefront16.hpp) or columns C
-                const int64_t kc = (int64_t)y8 + (GX_LOCAL_UKEY ? pl.G16 : 0);
+                // key range: steps C + G (wavefront16.hpp step_local_dr: keys rank steps)
+                const int64_t kc = (int64_t)y8 + pl.G16;
                 if (frame && (hmax + 1) * kc <= 0x7800) {
                     pl.kf16 = y8;
                 } else if (pl.tb) {
@@ -378,8 +370,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 } else if (seg_ok && kseg_mode == 2) {
                     pl.kf16 = y8;
                     pl.kseg_shift = mseg;
-                } else if (frame && (hmax + 1) * kc <= 0x10000 && y8 <= 0xFFFF &&
-                           env_flag("GASALX_KU16", true)) {
+                } else if (frame && (hmax + 1) * kc <= 0x10000 && y8 <= 0xFFFF) {
                     pl.kf16 = y8;
                     pl.ku16 = true;
                 } else if (seg_ok) {
@@ -522,15 +513,6 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
                                        (int)pl.lds16_bytes));
         hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
         HIPCHK(hipGetLastError());
-        if (pl.tb_band && !GX_TB_FUSED) {   // the band pass over the blocks the sweep aligned (same grid and slots)
-            WfFn fb = wf16_pick_r4<WF16_GLOBAL_BAND>(pl.G16, pl.R16);
-            if (!fb) { set_error("no packed band instance"); return GASALX_EUNSUPPORTED; }
-            if (pl.lds16_bytes > 64 * 1024)
-                HIPCHK(hipFuncSetAttribute((const void *)fb, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)pl.lds16_bytes));
-            hipLaunchKernelGGL(fb, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
-            HIPCHK(hipGetLastError());
-        }
         // ... and the int32 kernel aligns the pairs of the blocks it declined
         A.skip = ws.misc.as<uint8_t>();
         A.skip_ppb = ppb16;
@@ -716,23 +698,9 @@ static int geometry_perm(Workspace &ws, const gasalx_batch &b, const BatchShape 
 // Everything after align_device's prologue, over the pairs of b (a whole batch or one
 // chunk of it).  walk_qseq: the query codes the traceback walk reads when the CIGAR
 // buffer overlays the query batch (copied once by the prologue), else NULL.
-enum { PHASE_DP = 1, PHASE_WALK = 2, PHASE_ALL = 3 };
 static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, const gasalx_batch &b,
                       const gasalx_results &out, hipStream_t st, const BatchShape &shape, uint64_t cigar_cap,
-                      const uint8_t *walk_qseq, int phases = PHASE_ALL);
-
-// GASALX_TB_CHUNKS: chunks of a traceback batch (A/B runs; 1 = one launch pair)
-static uint32_t tb_chunks(uint32_t n) {
-    static const int force = [] {
-        const char *e = std::getenv("GASALX_TB_CHUNKS");
-        return e ? std::atoi(e) : 0;
-    }();
-    (void)n;
-    // default one launch pair: the walk is latency-bound (a 25 K-pair chunk's walk takes
-    // 0.51 ms, the whole 100 K-pair batch's 0.70 ms, profiles/r03_tb_chunks.md), so the
-    // last chunk's walk costs nearly the whole walk again and chunking only adds DP tails
-    return force > 0 ? (uint32_t)force : 1u;
-}
+                      const uint8_t *walk_qseq);
 
 int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, const gasalx_results &out,
                  hipStream_t st, const BatchShape &shape, uint64_t cigar_cap) {
@@ -772,120 +740,21 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         }
     }
 
-    // Traceback in chunks (GASALX_TB_CHUNKS > 1): the DP kernel is VALU-bound, the
-    // walk (tb_kernel) bound by the latency of its dependent loads.  Chunk k's DP runs
-    // on the caller's stream, its walk on a second stream after an event, beside the
-    // following DPs.  Every chunk has its own workspace (direction data, flags, ends).
-    // A chunk's walk writes CIGARs over the query bytes of its pairs while the next chunk's DP
-    // runs: when the CIGAR buffer is the query batch, every chunk's DP reads the copy taken
-    // above (pairs may share query bytes, one-to-many), and without a copy there is no split
-    const bool can_split = runs_tb && out.cigar && out.n_cigar_ops && shape.tb_split && pl.kind == PLAN_WAVEFRONT &&
-                           !pl.need_pack && (!cigar_on_query || walk_qseq);
-    // Tail split (GASALX_TB_TAIL=1, A/B): the pairs that fill whole rounds of the packed
-    // DP kernel's wave slots, then the rest.  Chunk 0's walk runs on the second stream
-    // beside chunk 1's DP (the DP's last, partly filled round), chunk 1's walk follows
-    // its DP on the caller's stream.
-    if (can_split && pl.packed16 && env_flag("GASALX_TB_TAIL", false)) {
-        int cus = 0;
-        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ws.device));
-        const uint32_t per_wave = 2u * (64u / (uint32_t)pl.G16), waves_simd = 2;   // GX_WF16_TB_WAVES / _LTB_WAVES
-        const uint64_t round = (uint64_t)cus * 4 * waves_simd * per_wave;
-        const uint32_t n0 = round ? (uint32_t)((n / round) * round) : 0;
-        if (n0 > 0 && n0 < n) {
-            if (ws.sides.empty()) ws.sides.push_back(new Workspace());
-            ws.sides[0]->device = ws.device;
-            if (!ws.walk_stream) HIPCHK(hipStreamCreateWithFlags(&ws.walk_stream, hipStreamNonBlocking));
-            for (hipEvent_t *x : {&ws.fork, &ws.join, &ws.dp_done})
-                if (!*x) HIPCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
-            HIPCHK(hipEventRecord(ws.fork, st));
-            HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.fork, 0));
-            int rc = GASALX_OK;
-            for (uint32_t c = 0; c < 2 && rc == GASALX_OK; c++) {
-                const uint32_t i0 = c ? n0 : 0, m = c ? n - n0 : n0;
-                gasalx_batch cb = b;
-                if (walk_qseq) cb.q_batch = walk_qseq;
-                cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
-                if (cb.q_ops) cb.q_ops += i0;
-                if (cb.t_ops) cb.t_ops += i0;
-                if (cb.seed_scores) cb.seed_scores += i0;
-                cb.n_alns = m;
-                gasalx_results co = out;
-                for (int32_t **f : {&co.aln_score, &co.q_end, &co.t_end, &co.q_start, &co.t_start, &co.aln_score2,
-                                    &co.q_end2, &co.t_end2})
-                    if (*f) *f += i0;
-                co.n_cigar_ops += i0;
-                BatchShape cs = sized;
-                cs.n = m;
-                const Plan cp = make_plan(p, cs, has_ops);
-                Workspace &w = c ? *ws.sides[0] : ws;
-                rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_DP);
-                if (rc) break;
-                if (c == 0) {
-                    HIPCHK(hipEventRecord(ws.dp_done, st));
-                    HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.dp_done, 0));
-                    rc = align_body(w, p, cp, cb, co, ws.walk_stream, cs, cigar_cap, walk_qseq, PHASE_WALK);
-                } else {
-                    rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_WALK);
-                }
-            }
-            HIPCHK(hipEventRecord(ws.join, ws.walk_stream));
-            HIPCHK(hipStreamWaitEvent(st, ws.join, 0));
-            return rc;
-        }
-    }
-    const uint32_t chunks = can_split ? tb_chunks(n) : 1;
-    if (chunks > 1) {
-        while (ws.sides.size() + 1 < chunks) ws.sides.push_back(new Workspace());
-        for (Workspace *w : ws.sides) w->device = ws.device;
-        if (!ws.walk_stream) HIPCHK(hipStreamCreateWithFlags(&ws.walk_stream, hipStreamNonBlocking));
-        for (hipEvent_t *x : {&ws.fork, &ws.join, &ws.dp_done})
-            if (!*x) HIPCHK(hipEventCreateWithFlags(x, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(ws.fork, st));
-        HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.fork, 0));
-        const uint32_t per = (n + chunks - 1) / chunks;
-        int rc = GASALX_OK;
-        for (uint32_t c = 0, i0 = 0; i0 < n && rc == GASALX_OK; c++, i0 += per) {
-            const uint32_t m = std::min(per, n - i0);
-            gasalx_batch cb = b;
-            if (walk_qseq) cb.q_batch = walk_qseq;
-            cb.q_offsets += i0; cb.t_offsets += i0; cb.q_lens += i0; cb.t_lens += i0;
-            if (cb.q_ops) cb.q_ops += i0;
-            if (cb.t_ops) cb.t_ops += i0;
-            if (cb.seed_scores) cb.seed_scores += i0;
-            cb.n_alns = m;
-            gasalx_results co = out;
-            for (int32_t **f : {&co.aln_score, &co.q_end, &co.t_end, &co.q_start, &co.t_start, &co.aln_score2,
-                                &co.q_end2, &co.t_end2})
-                if (*f) *f += i0;
-            co.n_cigar_ops += i0;      // the CIGAR buffer is addressed by query offsets
-            BatchShape cs = sized;
-            cs.n = m;
-            const Plan cp = make_plan(p, cs, has_ops);
-            Workspace &w = c ? *ws.sides[c - 1] : ws;
-            rc = align_body(w, p, cp, cb, co, st, cs, cigar_cap, walk_qseq, PHASE_DP);
-            if (rc) break;
-            HIPCHK(hipEventRecord(ws.dp_done, st));
-            HIPCHK(hipStreamWaitEvent(ws.walk_stream, ws.dp_done, 0));
-            rc = align_body(w, p, cp, cb, co, ws.walk_stream, cs, cigar_cap, walk_qseq, PHASE_WALK);
-        }
-        // join: the caller's stream continues after the walks
-        HIPCHK(hipEventRecord(ws.join, ws.walk_stream));
-        HIPCHK(hipStreamWaitEvent(st, ws.join, 0));
-        return rc;
-    }
+    // (one launch pair: the walk is latency-bound -- a 25 K-pair chunk's walk takes 0.51 ms, the
+    // whole 100 K-pair batch's 0.70 ms, profiles/r03_tb_chunks.md -- so chunking only added DP
+    // tails; round 4's chunk and tail-split paths measured no gain and are gone)
     return align_body(ws, p, pl, b, out, st, sized, cigar_cap, walk_qseq);
 }
 
 static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, const gasalx_batch &b,
                       const gasalx_results &out, hipStream_t st, const BatchShape &shape, uint64_t cigar_cap,
-                      const uint8_t *walk_qseq, int phases) {
-    const bool dp = phases & PHASE_DP;   // a walk-only call (chunked traceback) recomputes pointers, launches the walk
+                      const uint8_t *walk_qseq) {
     const bool has_ops = b.q_ops && b.t_ops;
     const uint32_t n = b.n_alns;
     const bool tb = p.start_pos == 2;
     const bool runs_tb = tb && (p.algo == 1 || p.algo == 3) && pl.kind != PLAN_NONE;
     if (pl.kind == PLAN_CONST) {
-        if (dp) semi_tail_none_kernel<<<grid_for(n, 256), 256, 0, st>>>(out.aln_score, out.q_end, out.t_end, b.q_lens,
+        semi_tail_none_kernel<<<grid_for(n, 256), 256, 0, st>>>(out.aln_score, out.q_end, out.t_end, b.q_lens,
                                                                       b.t_lens, n);
         HIPCHK(hipGetLastError());
         return GASALX_OK;
@@ -893,7 +762,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
 
     const uint8_t *qsrc = b.q_batch, *tsrc = b.t_batch;
     int packed = p.is_packed ? 1 : 0;
-    if (pl.need_pack) {   // (never in a walk-only call: chunked traceback excludes need_pack)
+    if (pl.need_pack) {
         const uint32_t qw = b.q_bytes / 8, tw = b.t_bytes / 8;
         HIPCHK(ws.packed_q.reserve((size_t)qw * 4 + 16));
         HIPCHK(ws.packed_t.reserve((size_t)tw * 4 + 16));
@@ -963,21 +832,18 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             if (2 * sh <= 64 * 1024) {
                 HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + (size_t)(s8w + 1) * 8 + 64));
                 uint32_t *perm = ws.sort_meta.as<uint32_t>(), *inv = perm + n, *hist = inv + n, *cursor = hist + s8w + 1;
-                if (dp) {
-                    HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-                    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
-                    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
-                    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w,
-                                                                              cursor, perm, inv);
-                    HIPCHK(hipGetLastError());
-                }
+                HIPCHK(hipMemsetAsync(hist, 0, sh, st));
+                rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
+                rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
+                rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w,
+                                                                          cursor, perm, inv);
+                HIPCHK(hipGetLastError());
                 A.perm = perm;
                 slot_of = inv;
             }
         }
         // unsorted waves hold consecutive pairs: interleave their direction chunks
-        // (GASALX_TB_Q8=0: per-pair layout, A/B)
-        A.tb_q8 = (pl.packed16 && pl.tb && !pl.tb_band && !A.perm && env_flag("GASALX_TB_Q8", true)) ? 1u : 0u;
+        A.tb_q8 = (pl.packed16 && pl.tb && !pl.tb_band && !A.perm) ? 1u : 0u;
         tb_q8 = A.tb_q8;
         if (pl.tb_band && runs_tb) {
             // band recomputation buffers per wave of the packed launch (wavefront16.hpp)
@@ -994,14 +860,14 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             A.band_wd = pl.band_wd;
             fb_count = ws.band_fb.as<uint32_t>();
         }
-        int rc = !dp ? GASALX_OK : pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st, shape.one_t8) : launch_wavefront(ws, pl, p, A, st);
+        int rc = pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st, shape.one_t8) : launch_wavefront(ws, pl, p, A, st);
         if (rc) return rc;
-        if (wf_start && dp) {
+        if (wf_start) {
             rc = start_reverse(ws, p.algo == 3 ? REV_LOCAL : REV_SEMI, p, qsrc, tsrc, packed, b, shape, out.aln_score,
                                qend, tend, out.q_start, out.t_start, st);
             if (rc) return rc;
         }
-    } else if (dp) {
+    } else {
         GenArgs A;
         std::memset(&A, 0, sizeof(A));
         A.qw = ws.packed_q.as<uint32_t>(); A.tw = ws.packed_t.as<uint32_t>();
@@ -1030,10 +896,9 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             const size_t ke = (size_t)(shape.max_q + 8) * n;
             HIPCHK(ws.rows_h.reserve(ke * 8));
             // 8-bit (h, e) entries, then 16-bit, then int2, each for the pairs whose score
-            // bound does not fit the level before (GASALX_KSW_NARROW=0: int2 only, A/B)
-            const char *kn = std::getenv("GASALX_KSW_NARROW");
+            // bound does not fit the level before
             uint8_t *todo = nullptr;
-            if (!(kn && std::atoi(kn) == 0)) {
+            {
                 HIPCHK(ws.misc.reserve(n));
                 HIPCHK(hipMemsetAsync(ws.misc.p, 0, n, st));
                 todo = ws.misc.as<uint8_t>();
@@ -1059,11 +924,9 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                     K.kofs = kofs;
                     // the entry row in registers when the padded query fits an instance
                     // (selector words in LDS: QC / 2 words per lane), else the global array
-                    // (GASALX_KSW16_REG=0: global, A/B)
                     int qc = 0;
-                    if (env_flag("GASALX_KSW16_REG", true))
-                        for (int c : {64, 96, 160})
-                            if (K.cols <= (uint32_t)c) { qc = c; break; }
+                    for (int c : {64, 96, 160})
+                        if (K.cols <= (uint32_t)c) { qc = c; break; }
                     if (qc) {
                         void (*fn)(Ksw16Args) = qc == 64 ? &ksw16_kernel<64> : qc == 96 ? &ksw16_kernel<96> : &ksw16_kernel<160>;
                         const size_t lds = (size_t)4 * (qc / 2) * 64 * 4;
@@ -1171,7 +1034,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         HIPCHK(hipGetLastError());
     }
 
-    if (runs_tb && out.cigar && out.n_cigar_ops && (phases & PHASE_WALK)) {
+    if (runs_tb && out.cigar && out.n_cigar_ops) {
         TbArgs T;
         T.tb = ws.tb.as<uint32_t>(); T.tb_pair_words = tb_words;
         T.qlen = b.q_lens; T.tlen = b.t_lens; T.qoff = b.q_offsets;
@@ -1242,10 +1105,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
 }
 
 // ----------------------------------------------------------------------------
-#ifndef GX_HMM_RR
-#define GX_HMM_RR 8   // read rows per lane (A/B: 16)
-#endif
-constexpr int kHmmRows = GX_HMM_RR;
+constexpr int kHmmRows = 8;   // read rows per lane
 using HmmFn = void (*)(HmmArgs);
 template <bool QUALS, bool ABS>
 static HmmFn hmm_lookup(int G) {
@@ -1259,33 +1119,6 @@ static HmmFn hmm_lookup(int G) {
     }
 }
 
-// Two problems per lane group (pairhmm2_kernel) with kHmm2Rows read rows per lane: the
-// lane holds as many cells as pairhmm_kernel's (2 x 4 = 8), so its registers stay at three
-// waves per SIMD, while the eight cells of a column issue as four packed fp32 ops each.
-// The group is twice as wide for the same read (G = 64 for 250 rows): 31 more fill/drain
-// steps.  GASALX_HMM2=0 keeps the one-problem kernel (A/B).  With 8 rows per lane
-// (-DGX_HMM2_RR=8) the kernel needs 254 VGPRs, 2 waves, and is slower
-// (profiles/r03_pairhmm_ab.md).
-#ifndef GX_HMM2_RR
-#define GX_HMM2_RR 4
-#endif
-constexpr int kHmm2Rows = GX_HMM2_RR;
-template <bool QUALS, bool ABS>
-static HmmFn hmm2_lookup(int G) {
-    switch (G) {
-        case 4: return &pairhmm2_kernel<4, kHmm2Rows, QUALS, ABS>;
-        case 8: return &pairhmm2_kernel<8, kHmm2Rows, QUALS, ABS>;
-        case 16: return &pairhmm2_kernel<16, kHmm2Rows, QUALS, ABS>;
-        case 32: return &pairhmm2_kernel<32, kHmm2Rows, QUALS, ABS>;
-        case 64: return &pairhmm2_kernel<64, kHmm2Rows, QUALS, ABS>;
-        default: return nullptr;
-    }
-}
-static bool hmm2_wanted() {
-    static const bool on = env_flag("GASALX_HMM2", false);
-    return on;
-}
-
 // lanes per pair for a read of max_r rows: `rows` read rows per lane, G in {4, ..., 64}
 static int hmm_group(uint32_t max_r, int rows) {
     for (int g : {4, 8, 16, 32, 64})
@@ -1297,9 +1130,7 @@ int pairhmm_group(uint32_t max_r) { return hmm_group(max_r, kHmmRows); }
 // One launch over slots [slot0, slot1) of A (A.perm maps slots to pairs, or NULL).
 static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0, uint32_t slot1, uint32_t max_h,
                           hipStream_t st) {
-    // two problems per group where the read fits 64 x kHmm2Rows rows
-    const int per_group = hmm2_wanted() && hmm_group(max_r, kHmm2Rows) ? 2 : 1;
-    const int rows = per_group == 2 ? kHmm2Rows : kHmmRows;
+    const int rows = kHmmRows;
     const int G = hmm_group(max_r, rows);
     if (slot1 <= slot0) return GASALX_OK;
     if (!G) { set_error("PairHMM read longer than 512"); return GASALX_ERANGE; }
@@ -1310,17 +1141,13 @@ static int pairhmm_launch(HmmArgs A, bool quals, uint32_t max_r, uint32_t slot0,
     // absorbs the boundary (pairhmm.hpp ABS)
     const bool absorb = (uint32_t)G * rows > max_r;
     // haplotype slots, then the per-lane prior tables (pairhmm.hpp): 4 waves x 4 codes x
-    // rows x 64 lanes x 4 bytes, per problem of a lane group
-    const size_t lds = (((size_t)4 * per_group * (64 / G) * A.lds_stride + 15) & ~(size_t)15) +
-                       (size_t)per_group * 4 * 4 * rows * 64 * 4 +
-                       (GX_HMM_CODE16 && per_group == 1 ? (size_t)4 * (64 / G) * A.lds_stride * 2 + 16 : 0);
+    // rows x 64 lanes x 4 bytes
+    const size_t lds = (((size_t)4 * (64 / G) * A.lds_stride + 15) & ~(size_t)15) + (size_t)4 * 4 * rows * 64 * 4;
     if (lds > 160 * 1024) { set_error("PairHMM haplotype too long"); return GASALX_ERANGE; }
-    HmmFn fn = per_group == 2 ? (quals ? (absorb ? hmm2_lookup<true, true>(G) : hmm2_lookup<true, false>(G))
-                                       : (absorb ? hmm2_lookup<false, true>(G) : hmm2_lookup<false, false>(G)))
-                              : (quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
-                                       : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G)));
+    HmmFn fn = quals ? (absorb ? hmm_lookup<true, true>(G) : hmm_lookup<true, false>(G))
+                     : (absorb ? hmm_lookup<false, true>(G) : hmm_lookup<false, false>(G));
     if (lds > 64 * 1024) HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * per_group * (64 / G))), dim3(256), lds, st, A);
+    hipLaunchKernelGGL(fn, dim3(grid_for(slot1 - slot0, 4 * (64 / G))), dim3(256), lds, st, A);
     HIPCHK(hipGetLastError());
     return GASALX_OK;
 }

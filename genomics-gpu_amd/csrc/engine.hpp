@@ -40,12 +40,6 @@ struct Workspace {
     // the last packed launch's "aligned here" flags in misc (gasalx_packed_pairs): flag count, pairs
     // per flag, pairs of the launch (0 flags: no packed launch yet)
     uint32_t pk_flags = 0, pk_ppb = 0, pk_pairs = 0;
-    // traceback batches in chunks (align_device, GASALX_TB_CHUNKS): DPs on the
-    // caller's stream, walks on walk_stream; one workspace per further chunk; all
-    // created on first use
-    hipStream_t walk_stream = nullptr;
-    std::vector<Workspace *> sides;
-    hipEvent_t fork = nullptr, join = nullptr, dp_done = nullptr;
     void release_all();
 };
 

@@ -584,7 +584,7 @@ struct TbArgs {
     const uint8_t *qseq, *tseq;
     const uint32_t *toff;
     int32_t seq_packed, nval, has_npen, npen;
-    // band recomputation (wavefront16.hpp WF16_GLOBAL_BAND): packed pairs read the flags of
+    // band recomputation (wavefront16.hpp WF16_GLOBAL_CP band pass): packed pairs read the flags of
     // their lane's band window ([wave][64][wd/4][R/4] uint4, two pairs per entry); a path that
     // leaves the band appends its pair to fb_list and stops (its bytes so far are a prefix of
     // the CIGAR the full-matrix walk writes later)

@@ -54,7 +54,7 @@ struct WfArgs {
     const int32_t *stop;       // SEMI TAIL=TARGET reverse pass (start.hpp): per pair, the forward score; the
                                // last-row maximum is then taken inside the first 8-column strip holding a
                                // value >= it (the reference's early exit), else over the whole row
-    // GLOBAL + traceback by band recomputation (wavefront16.hpp WF16_GLOBAL_CP / WF16_GLOBAL_BAND):
+    // GLOBAL + traceback by band recomputation (wavefront16.hpp WF16_GLOBAL_CP, sweep then band pass):
     // per wave, the left-edge state of every lane's band window (cp: [wave][64][2R] words) and the
     // bottom-row hand-off of every lane over the window of the lane below (stm: [wave][wd+1][64]),
     // then the band's direction flags (bflags: [wave][64 lanes][wd/4 windows][R/4] uint4)

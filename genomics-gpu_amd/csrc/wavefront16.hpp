@@ -79,36 +79,12 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
     return GX_AS(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
 
-#ifndef GX_SEMI_CHAIN2
-#define GX_SEMI_CHAIN2 0   // step_semi A/B (see there)
-#endif
-#ifndef GX_PROBE_LOCAL
-#define GX_PROBE_LOCAL 0   // step_local timing probes (bit 0: F, bit 1: E without the extension subtract)
-#endif
-#ifndef GX_WF16_TB_INPLACE
-#define GX_WF16_TB_INPLACE 0
-#endif
-#ifndef GX_WF16_TB_WAVES
-#define GX_WF16_TB_WAVES 2   // GLOBAL + traceback kernel
-#endif
-#ifndef GX_TB_STORE_MODE
-#define GX_TB_STORE_MODE 0   // GLOBAL+TB direction stores (1: no-store timing probe, r02_tb_store_ab.md)
-#endif
-#ifndef GX_WF16_TB_ROWSYNC
-#define GX_WF16_TB_ROWSYNC 0
-#endif
+constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
-#ifndef GX_LOCAL_UKEY
-#define GX_LOCAL_UKEY 1   // LOCAL e-drift keys with wave-uniform addends (0: per-lane subtracts, A/B)
-#endif
-#ifndef GX_WF16_K2_WAVES
-#define GX_WF16_K2_WAVES 2    // LOCAL over 257..512 target columns (a 3-wave build spills)
-#endif
-#ifndef GX_WF16_LTB_WAVES
-#define GX_WF16_LTB_WAVES 2   // LOCAL + traceback kernel
-#endif
+constexpr int kW16_K2_WAVES = 2;    // LOCAL over 257..512 target columns (a 3-wave build spills)
+constexpr int kW16_LTB_WAVES = 2;   // LOCAL + traceback kernel
 
 // A/C/G/T nibble -> 0..3, N -> 4, anything else -> 5
 __device__ __forceinline__ uint32_t letter_of(uint32_t nib, int32_t nval) {
@@ -193,16 +169,8 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
         const uint32_t tmp = pk_subnb(t1, KK);
         const uint32_t toe = pk_subnb(t1, OEK);
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
-#if GX_PROBE_LOCAL & 2   // timing probes only (results invalid): no E / F extension subtract
-        Ek[k] = pk_max3(toe, Ek[k], BB);
-#else
         Ek[k] = pk_max3(toe, pk_subnb(Ek[k], EXT), BB);
-#endif
-#if GX_PROBE_LOCAL & 1
-        f = pk_max3(toe, f, BB);
-#else
         f = pk_max3(toe, pk_subnb(f, EXT), BB);
-#endif
         if (KU == 2) key[k] = pk_max3(key[k], pk_mad_u16(Hin[k], KMUL, invp), pk_mad_u16(H, KMUL, invn));
         if (KU == 0 && KM != 2) key[k] = pk_max_u16(key[k], pk_mad_u16(H, kmA, invc));
         if (KU == 0 && KM != 0) key2[k] = pk_max_u16(key2[k], pk_mad_u16(H, kmB, invc2));
@@ -235,11 +203,9 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                                               const uint32_t EXT, const uint32_t KMUL, const uint32_t invp,
                                               const uint32_t invn, const uint32_t EXT2, const uint32_t MK16 = 0) {
     uint32_t diag = diag_top, f = f_top;
-#if GX_LOCAL_UKEY
     // row 0's addends (invp / invn: the candidates' bases), then one scalar subtract per row
     const uint32_t g20 = (FL[0] - EXT2) & 0xFFFFu, EM = (EXT2 >> 1 & 0xFFFFu) * MK16;   // e * M
     uint32_t a1 = invp - g20 * MK16, a2 = invn - g20 * MK16;
-#endif
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
@@ -249,7 +215,6 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
         const uint32_t H = pk_max3(tmp, f, Ek[k]);
         Ek[k] = pk_max3(toe, Ek[k], FL[k]);
         if (KEYS) {
-#if GX_LOCAL_UKEY
             // key = (H^ - g2) * M + base = H^ * M + (base - g2 * M) (mod 2^16): the addend is the
             // same in every lane (FL and the step's bases are wave-uniform), so it is scalar work
             // and a cell pair's keys cost two mads and one max (the subtracts are gone)
@@ -259,15 +224,6 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                 key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
             a1 -= EM;   // row k + 1: FL one e higher
             a2 -= EM;
-#else
-            // 32-bit subtracts, borrow-free: Hin >= FL - 2e and H >= FL - e
-            const uint32_t g2 = pk_subnb(FL[k], EXT2);
-            const uint32_t d1 = pk_subnb(Hin[k], g2), d2 = pk_subnb(H, g2);
-            if (U16)
-                key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn)));
-            else
-                key[k] = pk_max3(key[k], pk_mad_u16(d1, KMUL, invp), pk_mad_u16(d2, KMUL, invn));
-#endif
         }
         FL[k] = pk_addnc(FL[k], EXT);
         f = pk_max_u16(toe, f);
@@ -319,21 +275,14 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
 //   u = [H != tmp], w = [H != F], x = [toe > E - e], y = [toe > F - e]
 // (x, y are the reference's own "not extended" tests).  A flag is bit 15 of the
 // per-half difference B - A (one v_pk_sub_u16): [A != B] for A >= B, [A > B] for
-// |A - B| < 0x7800 (GX_TB_FLAG_ADD 1: the round-2 form, (A + 0x7FFF) - B as two
+// |A - B| < 0x7800 (round 2 used (A + 0x7FFF) - B as two
 // 32-bit ops with no carry/borrow across a half, 6 instructions for 4 flags instead
 // of 4); v_perm's sign selectors turn two such bits into 0x00/0xFF bytes and one
 // v_and_or places them: step j of a 4-step window owns bits j (u), 4+j (w),
 // 8+j (x) and 12+j (y) of each 16-bit half of dw.
 // ---------------------------------------------------------------------------
-#ifndef GX_TB_FLAG_ADD
-#define GX_TB_FLAG_ADD 0
-#endif
 __device__ __forceinline__ uint32_t tb_flag(uint32_t a, uint32_t b) {
-#if GX_TB_FLAG_ADD
-    return (a + 0x7FFF7FFFu) - b;
-#else
     return GX_AS(uint32_t, GX_AS(pk_u2, b) - GX_AS(pk_u2, a));
-#endif
 }
 // (a & m) | b as one v_bitop3_b32 (truth table 0xEA); the compiler would
 // otherwise split the two merges of a row into and, and, or3
@@ -349,7 +298,7 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
 // With F unfloored, w and y are the reference's own tests on every cell; x differs from the
 // reference only where E is floored (E <= 0), never on a gap run the walk follows (it stops
 // before H = 0, get_tb.h:100-103).  Keys: the wave-uniform addends of step_local_dr
-// (GX_LOCAL_UKEY), two columns per v_pk_maximum3 on the KEYS steps.  15.5 instructions per cell
+// (step_local_dr), two columns per v_pk_maximum3 on the KEYS steps.  15.5 instructions per cell
 // pair instead of step_local_tb's 19.
 // ---------------------------------------------------------------------------
 template <int R, bool KEYS>
@@ -424,9 +373,6 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
         f = Fn;
         diag = Hin[k];
         Hout[k] = H;
-#if GX_WF16_TB_ROWSYNC
-        asm volatile("" : "+v"(f), "+v"(tx), "+v"(ty));   // schedule row by row (tuning variant)
-#endif
         // SYNC: each row's flags before the next row (the band pass deferred them all to the
         // window's store otherwise: 345 spilled VGPRs; 120 VGPRs with it)
         if (SYNC) asm volatile("" : "+v"(dw[k]), "+v"(f));
@@ -494,24 +440,6 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
                                           const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                           uint32_t (&Fk)[R], const uint32_t GO, const uint32_t *pv = nullptr) {
     uint32_t diag = diag_top, h = hl, e = el;
-#if GX_SEMI_CHAIN2
-    // timing A/B: E(r,c) = max(h, e) taken inside the next max3 as a fourth operand, so
-    // the dependency chain per register is sub + max3 instead of max + max3 + sub
-    // (one more instruction per two cells: max(tmp, F) off the chain)
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
-        if (PV > 0 && k >= R - PV) v = pk_addnc(v, pv[k - (R - PV)]);
-        const uint32_t tmp = pk_addnc(diag, v);
-        Fk[k] = pk_max_u16(Hin[k], Fk[k]);
-        const uint32_t a = pk_max_u16(tmp, Fk[k]);
-        const uint32_t en = pk_max_u16(h, e);                        // E(r,c), off the chain
-        h = pk_subnb(pk_max3(a, h, e), GO);                          // max3(tmp, F, max(h, e)) - o
-        e = en;
-        diag = Hin[k];
-        Hout[k] = h;
-    }
-#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
@@ -523,7 +451,6 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
         diag = Hin[k];
         Hout[k] = h;
     }
-#endif
     hl = h;
     el = e;
 }
@@ -583,17 +510,17 @@ constexpr int WF16_SEMI_TQ = 6;       // SEMI with TAIL = QUERY / BOTH: the last
 //  * WF16_GLOBAL_CP: the score-only GLOBAL sweep (step_global, no flags) that also stores, for
 //    every lane lg, its R rows' (H, E) at the column left of its band window [L, L + wd), L =
 //    max(lg*R - w, 0), and its bottom row's hand-off (H, F) over the window of the lane below;
-//  * WF16_GLOBAL_BAND: every lane recomputes its R x wd window from those values alone, with
-//    the direction flags of step_global_tb (identical inputs, identical flags), one 4-column
-//    window of flags at a time into bflags.  tb_kernel walks the band and hands the pairs whose
-//    path leaves it to a WF16_GLOBAL_TB launch over the full matrix (dispatch.hip).
+//  * then, in the same kernel (band_pass), every lane recomputes its R x wd window from those
+//    values alone, with the direction flags of step_global_tb (identical inputs, identical
+//    flags), one 4-column window of flags at a time into bflags.  tb_kernel walks the band and
+//    hands the pairs whose path leaves it to a WF16_GLOBAL_TB launch over the full matrix
+//    (dispatch.hip).
 // Per cell pair the sweep issues 7 instructions instead of step_global_tb's 15; the band is
 // R x wd of every lane's G*R x (ypad) cells (config 3, w = 12: 44 of 304 columns).
 // entries per lane of the band hand-off stream: wd + 1 used, rounded up to blocks of 4, plus the
 // two blocks the band pass prefetches past its last one
 __host__ __device__ constexpr uint32_t band_stream_words(uint32_t wd) { return ((wd + 1 + 3) & ~3u) + 8; }
 constexpr int WF16_GLOBAL_CP = 7;
-constexpr int WF16_GLOBAL_BAND = 8;
 // SEMI TAIL=TARGET reverse pass of WITH_START (start.hpp, A.stop): the forward instances keep
 // no stop branch, whose per-column constants the compiler hoisted out of the sweep and spilled
 // (config 4: 32 B of scratch per lane, 0.73 GB of traffic per launch)
@@ -608,40 +535,23 @@ constexpr int WF16_LOCAL_U16_RS = 12; // the same with u16 keys (local_rs.hip in
 // row the first segment holding its maximum (later columns win only when strictly higher)
 constexpr int WF16_LOCAL_SEG = 13;
 constexpr int WF16_LOCAL_TBD = 14;    // LOCAL + traceback in the e-drift frame (step_local_tb_dr)
-#ifndef GX_WF16_LTBD_WAVES
-#define GX_WF16_LTBD_WAVES 2
-#endif
-#ifndef GX_WF16_TQ_WAVES
-#define GX_WF16_TQ_WAVES 3
-#endif
-#ifndef GX_WF16_TQ_BIG_WAVES
-#define GX_WF16_TQ_BIG_WAVES 3   // R > 20 (A/B knob): 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
-#endif
-
-#ifndef GX_TB_FUSED
-#define GX_TB_FUSED 1   // GLOBAL+TB: the band pass inside the checkpoint sweep's kernel (0: its own launch)
-#endif
-#ifndef GX_WF16_CP_WAVES
-#define GX_WF16_CP_WAVES 3    // GLOBAL score sweep with band checkpoints
-#endif
-#ifndef GX_WF16_BAND_WAVES
-#define GX_WF16_BAND_WAVES 3  // band recomputation with flags (136 VGPRs with the stream blocks in flight)
-#endif
+constexpr int kW16_LTBD_WAVES = 2;
+constexpr int kW16_TQ_WAVES = 3;
+constexpr int kW16_TQ_BIG_WAVES = 3;   // R > 20: 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
+constexpr int kW16_CP_WAVES = 3;    // GLOBAL score sweep with band checkpoints, then its band pass
 
 template <int ALGO_, int G, int R>
-__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
-                                   : ALGO_ == WF16_LOCAL_TB ? GX_WF16_LTB_WAVES
-                                   : ALGO_ == WF16_LOCAL_TBD ? GX_WF16_LTBD_WAVES
-                                   : ALGO_ == WF16_LOCAL_K2 ? GX_WF16_K2_WAVES
-                                   : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? GX_WF16_TQ_BIG_WAVES : GX_WF16_TQ_WAVES)
-                                   : ALGO_ == WF16_GLOBAL_CP ? GX_WF16_CP_WAVES
-                                   : ALGO_ == WF16_GLOBAL_BAND ? GX_WF16_BAND_WAVES
+__global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? kW16_TB_WAVES
+                                   : ALGO_ == WF16_LOCAL_TB ? kW16_LTB_WAVES
+                                   : ALGO_ == WF16_LOCAL_TBD ? kW16_LTBD_WAVES
+                                   : ALGO_ == WF16_LOCAL_K2 ? kW16_K2_WAVES
+                                   : ALGO_ == WF16_SEMI_TQ ? (R > 20 ? kW16_TQ_BIG_WAVES : kW16_TQ_WAVES)
+                                   : ALGO_ == WF16_GLOBAL_CP ? kW16_CP_WAVES
                                    : GX_WF16_WAVES) void wf16_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr bool GTB = ALGO_ == WF16_GLOBAL_TB;
     constexpr bool GCP = ALGO_ == WF16_GLOBAL_CP;
-    constexpr bool GBD = ALGO_ == WF16_GLOBAL_BAND;
-    constexpr bool GT = GTB || GCP || GBD;   // the traceback kernels' declines and start-cell capture
+    constexpr bool GT = GTB || GCP;   // the traceback kernels' declines and start-cell capture
     constexpr bool LTB = ALGO_ == WF16_LOCAL_TB;
     constexpr bool K2 = ALGO_ == WF16_LOCAL_K2;
     constexpr bool KU16 = ALGO_ == WF16_LOCAL_U16 || ALGO_ == WF16_LOCAL_U16_RS;
@@ -696,38 +606,74 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     const uint32_t words = A.lds_stride >> 3;            // positions per slot, >= ymaxw + 2G + 4, multiple of 4
     uint2 *wl = reinterpret_cast<uint2 *>(lds) + (size_t)wave * S * words;
     bool other = false;                                  // a code the packed path cannot score
-    for (uint32_t base = 0; base < S * (words >> 2); base += 64) {
-        const uint32_t idx = base + lane;
-        const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
-        const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;   // first position of this quad
-        uint32_t tab[2][4];
+    // Every global load of the prologue is issued before any is used: loads inside per-row or
+    // per-quad conditionals compiled to one load + s_waitcnt vmcnt(0) each, i.e. ~50 serialised
+    // memory latencies per wave before its sweep (config 2: R = 19 rows x 2 pairs, 6 staging
+    // rounds x 2).  (The loads stay predicated -- a batch of empty sequences has no bytes to read --
+    // but nothing reads their values before the last one is issued.)
+    constexpr int CH = 8;                                // staging rounds whose loads are in flight together
+    const uint32_t quads = S * (words >> 2);
+    for (uint32_t base0 = 0; base0 < quads; base0 += 64 * CH) {
+        uint32_t v[CH][2], yl_[CH][2];
+        bool in_[CH][2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
-            const uint32_t ylen = __shfl(yl[h], ps * G);
-            uint32_t v = 0;
-            const bool in = (int32_t)y0 >= 0 && y0 < yp;
-            if (in) v = load4_codes_dir(A, Y, yof, ylen, y0 >> 2);
+        for (int it = 0; it < CH; ++it) {
+            const uint32_t idx = base0 + it * 64 + lane;
+            const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
+            const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;   // first position of this quad
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t l = in ? letter_of((v >> (8 * j)) & 15u, A.nval) : 6u;
-                other |= l == 5;
-                // traceback reads the first pad query row, scored here as -K: exact for
-                // pad x base columns, not for pad x real-N columns (N == N is a match)
-                if (GT && !A.has_npen) other |= l == 4 && y0 + j < ylen;
-                if (GT) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
-                tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
+                yl_[it][h] = __shfl(yl[h], ps * G);
+                in_[it][h] = (int32_t)y0 >= 0 && y0 < yp && idx < quads;
+                v[it][h] = in_[it][h] ? load4_codes_dir(A, Y, yof, yl_[it][h], y0 >> 2) : 0u;
             }
         }
-        if (idx < S * (words >> 2)) {
-            uint2 *dst = wl + ps * words + 4 * (idx - ps * (words >> 2));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) dst[j] = make_uint2(tab[0][j], tab[1][j]);
+        for (int it = 0; it < CH; ++it) {
+            const uint32_t idx = base0 + it * 64 + lane;
+            const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
+            const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;
+            uint32_t tab[2][4];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const bool in = in_[it][h];
+                const uint32_t ylen = yl_[it][h];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t l = in ? letter_of((v[it][h] >> (8 * j)) & 15u, A.nval) : 6u;
+                    other |= l == 5;
+                    // traceback reads the first pad query row, scored here as -K: exact for
+                    // pad x base columns, not for pad x real-N columns (N == N is a match)
+                    if (GT && !A.has_npen) other |= l == 4 && y0 + j < ylen;
+                    if (GT) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
+                    tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
+                }
+            }
+            if (idx < quads) {
+                uint2 *dst = wl + ps * words + 4 * (idx - ps * (words >> 2));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[j] = make_uint2(tab[0][j], tab[1][j]);
+            }
         }
     }
     // ---- register-axis letters: selector bytes 0 / 2 (0x0C = constant 0 outside) ----
     const uint32_t r0 = lg * R;
     uint32_t xs[R];
+    uint32_t xb[2][R];                                   // the rows' bytes (or packed words), loaded first
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t r = r0 + k;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            // (WITH_START reverse pass: position r of "the first xl bases, reversed", N past xl)
+            const bool ld = valid[h] && r < xpad[h] && !(A.rev && r >= xl[h]);
+            const uint32_t pos = A.rev ? xl[h] - 1u - r : r;
+            xb[h][k] = !ld ? 0u
+                       : A.packed ? reinterpret_cast<const uint32_t *>(X)[(xo[h] >> 3) + (pos >> 3)]
+                                  : (uint32_t)X[xo[h] + pos];
+        }
+    }
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t r = r0 + k;
@@ -735,11 +681,10 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (valid[h] && r < xpad[h]) {
-                // (WITH_START reverse pass: position r of "the first xl bases, reversed", N past xl)
                 const uint32_t pos = A.rev ? xl[h] - 1u - r : r;
                 const uint32_t cde = A.rev && r >= xl[h] ? (uint32_t)A.nval
-                                     : A.packed ? (load4_codes(X, xo[h], pos >> 2, 1) >> (8 * (pos & 3))) & 15u
-                                                : (uint32_t)X[xo[h] + pos] & 15u;
+                                     : A.packed ? (xb[h][k] >> (28 - 4 * (pos & 7))) & 15u
+                                                : xb[h][k] & 15u;
                 const uint32_t l = letter_of(cde, A.nval);
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T
@@ -773,7 +718,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 if (valid[h]) A.handled[pair0 + 2 * slot + h] = fast ? 1 : 0;
-    } else if (threadIdx.x == 0 && !GBD) {               // (the band pass repeats its sweep's verdict)
+    } else if (threadIdx.x == 0) {
         A.handled[blockIdx.x] = fast ? 1 : 0;
     }
     if (!fast) return;                                   // the int32 kernel takes this block
@@ -787,13 +732,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
     const bool top = lg == 0;
     int32_t c = -(int32_t)lg;                            // step-axis position of this lane
 
-    // Band recomputation (WF16_GLOBAL_BAND, or the sweep kernel itself once its sweep is done,
-    // GX_TB_FUSED): lane lg's rows r0..r0+R-1 over the columns [L, L + wd), L = max(r0 - w, 0),
-    // from the state the WF16_GLOBAL_CP sweep stored (same frame, same tables, so
-    // step_global_tb sees the inputs the full traceback sweep would).
     auto band_pass = [&]() __attribute__((always_inline)) {
-      if constexpr (GBD || GCP) {
-        // Band recomputation (WF16_GLOBAL_BAND): lane lg's rows r0..r0+R-1 over the columns
+      if constexpr (GCP) {
+        // Band recomputation (the WF16_GLOBAL_CP kernel once its sweep is done): lane lg's rows r0..r0+R-1 over the columns
         // [L, L + wd), L = max(r0 - w, 0), from the state WF16_GLOBAL_CP stored (same frame,
         // same tables, so step_global_tb sees the inputs the full traceback sweep would).
         // Entering column L: H(r, L - 1) and E(r, L) of the lane's rows (the left boundary of
@@ -859,10 +800,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         }
       }
     };
-    if constexpr (GBD) {
-        band_pass();
-        return;
-    }
 
     if (ALGO == WF_LOCAL) {
         const uint32_t KK = pk_bcast(P.k), OEK = pk_bcast(A.o + A.e + P.k);
@@ -938,9 +875,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 // column -1 as the left boundary H = E = 0.  Top lane: diag H(-1, c-1) = 0,
                 // F(0, c) <= 0 (BB).
                 const uint32_t C = A.kf16;
-                // key multiplier: KSEG's segment length M, else the step range C + G (GX_LOCAL_UKEY:
+                // key multiplier: KSEG's segment length M, else the step range C + G (
                 // keys rank steps, not columns, so that their addend is wave-uniform) or C
-                const uint32_t CP = GX_LOCAL_UKEY ? C + G : C;
+                const uint32_t CP = C + G;
                 const uint32_t MK = KSEG ? (1u << A.kseg_shift) : CP, KMC = A.one * MK;
                 const int32_t ge = A.e, pbv = P.base;
                 const uint32_t EXT2 = pk_bcast(2 * ge);
@@ -948,27 +885,14 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                                OEXD = (uint32_t)((P.k - 2 * ge + A.o) * 0x10001);
                 constexpr uint32_t KOFS = KU16 ? 0u : 0x0400u;   // u16 keys need no f16 offset
                 uint32_t segend = MK;                            // KSEG: the current segment's end step
-#if GX_LOCAL_UKEY
                 uint32_t KMV = KMC;
                 asm volatile("" : "+v"(KMV));   // the multiplier in a VGPR: the mads' scalar operand is the addend
-#else
-                const uint32_t KMV = KMC;
-#endif
-#if GX_LOCAL_UKEY
                 // the key base of the candidate at step ss: KOFS + (end - 1 - ss) + add * M, end = the
                 // segment's end step (KSEG) or C + G; the garbage columns left of the matrix hold H = 0
                 // and those right of it less than the maximum, so no column test is needed
                 auto inv = [&](uint32_t ss, uint32_t add) __attribute__((always_inline)) {
                     return (KOFS + ((KSEG ? segend : CP) - 1u - ss) + add * MK) & 0xFFFFu;
                 };
-#else
-                auto inv = [&](int32_t cc, uint32_t add) __attribute__((always_inline)) {
-                    const uint32_t term = !(cc >= 0 && (uint32_t)cc < C) ? 0u
-                                          : KSEG ? segend - 1u - (uint32_t)(cc + (int32_t)lg)   // the step's rank
-                                                 : C - 1u - (uint32_t)cc;
-                    return ((KOFS + term + add * MK) & 0xFFFFu) * 0x10001u;
-                };
-#endif
                 // Each lane keeps the frame shifted by its own constant, e(k + s) instead of
                 // e(r + c) (r = lg*R + k, c = s - lg): every floor FL[k] = B + e(k + s + 1) is
                 // then the same in all lanes (scalar registers, s_add per step) and the
@@ -996,7 +920,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
                     for (int h = 0; h < 2; ++h) sstop[h] = valid[h] ? A.lstop[pr[h]] : 0;
                 }
-#if GX_LOCAL_UKEY
                 if constexpr (LTBD) {
                     // four steps per window of direction flags (tb_store_window, the LOCAL_TB layout);
                     // the keys of two columns on the second step of each pair
@@ -1029,7 +952,6 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                         tb_store_window<G, R>(A, pr, valid, W16, s >> 2, lg, dw);   // layout: see tb_store_window
                     }
                 }
-#endif
                 for (; !LTBD && s < nsteps; s += 2, c += 2) {
                     if (KSEG && s == segend && jseg < A.kseg_n) {   // wave-uniform: a segment ends
                         // [wave][segment][lane][R]: one base address, immediate offsets
@@ -1050,13 +972,8 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     T = tnext;
                     tnext = tcol[c + 2 + G];
                     const uint32_t dt1 = (uint32_t)(pbv + ge * (c - 1)) * 0x10001u;
-#if GX_LOCAL_UKEY
                     step_local_dr<R, true, KU16>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
                                            KXD, OEXD, EXT, KMV, inv(s, 0), inv(s + 1, (uint32_t)(-ge)), EXT2, MK);
-#else
-                    step_local_dr<R, true, KU16>(T, top ? dt1 : prevRecvH, top ? BB : recvF, xs, HB, HA, Ek, key, FL, f,
-                                           KXD, OEXD, EXT, KMC, inv(c, 0), inv(c + 1, (uint32_t)(-ge)), EXT2);
-#endif
                     prevRecvH = recvH;
                     recvH = pk_subnb((uint32_t)shr_lane((int32_t)HA[R - 1]), ADJ);
                     recvF = pk_subnb((uint32_t)shr_lane((int32_t)f), ADJ);
@@ -1070,9 +987,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                             bool hit[2];
 #pragma unroll
                             for (int h = 0; h < 2; ++h) {
-                                // (the key of column m: step m + lg, GX_LOCAL_UKEY; else column m)
+                                // (the key of column m: step m + lg)
                                 const uint32_t thr = KOFS + (uint32_t)sstop[h] * MK +
-                                                     (GX_LOCAL_UKEY ? CP - 1u - (uint32_t)m - lg : C - 1u - (uint32_t)m);
+                                                     (CP - 1u - (uint32_t)m - lg);
                                 hit[h] = !valid[h] || sstop[h] <= 0 || ((mx >> (16 * h)) & 0xFFFFu) >= thr;
                             }
                             if (groups_all<G>(__ballot(hit[0])) && groups_all<G>(__ballot(hit[1]))) break;
@@ -1094,9 +1011,9 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
         // above them in the lane, and tie it only in a later row of the same or a later strip.
         uint64_t bestv[2] = {0, 0};
         static_assert(R <= 32, "row index of the merge codes: 5 bits");
-        const bool fastkey = !K2 && !LTB && !KSEG && A.kf16 && A.kf16 + (GX_LOCAL_UKEY ? G : 0) <= 2048;   // strip: 8 bits
+        const bool fastkey = !K2 && !LTB && !KSEG && A.kf16 && A.kf16 + G <= 2048;   // strip: 8 bits
         if (fastkey) {
-            const uint32_t C = A.kf16 + (GX_LOCAL_UKEY ? G : 0);
+            const uint32_t C = A.kf16 + G;
             constexpr uint32_t KOFS_ = KU16 ? 0u : 0x0400u;
             uint32_t km = key[0];
 #pragma unroll
@@ -1107,7 +1024,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                 Hm[h] = (((km >> (16 * h)) & 0xFFFFu) - KOFS_) / C;
                 thr |= (KOFS_ + Hm[h] * C) << (16 * h);
             }
-            const uint32_t cb = pk_bcast((int32_t)(C - 1u - (GX_LOCAL_UKEY ? lg : 0u)));   // col = cb - (key - thr)
+            const uint32_t cb = pk_bcast((int32_t)(C - 1u - lg));   // col = cb - (key - thr)
             const pk_u2 one = {1, 1}, ffff = {0xFFFF, 0xFFFF};
             uint32_t bc = 0xFFFFFFFFu;
 #pragma unroll
@@ -1315,11 +1232,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
                     half_step(flg, c + 1, 1, HB, HA);
                     half_step(flg, c + 2, 2, HA, HB);
                     half_step(flg, c + 3, 3, HB, HA);
-#if GX_TB_STORE_MODE == 1
-                    asm volatile("" ::"v"(dw[0]), "v"(dw[R - 1]));   // timing probe only: no direction stores
-#else
                     tb_store_window<G, R>(A, pr, valid, W16, s >> 2, lg, dw);   // layout: see tb_store_window
-#endif
                 } else {
                     half_step(flg, c, 0, HA, HB);
                     half_step(flg, c + 1, 1, HB, HA);
@@ -1347,7 +1260,7 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? GX_WF16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             if (valid[h] && lg == kq_lane[h]) A.score[pr[h]] = score[h];
-        if constexpr (GCP && GX_TB_FUSED) {
+        if constexpr (GCP) {
             // the band pass right behind the sweep, in the same wave: no second prologue, and the
             // checkpoints and hand-offs just written (this wave's own stores) are read from L2
             __threadfence_block();

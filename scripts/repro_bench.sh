@@ -1,11 +1,11 @@
 #!/bin/bash
-# round 4, final library: the bench line of every workload with its CPU baseline, end-to-end
+# the bench line of every workload with its CPU baseline, end-to-end
 # columns and parity (bench.py picks up profiles/pmc_<w>.json of the same library and plan).
-# Output: gpurun_out/r04final/bench_<w>.json
+# Output: gpurun_out/$REPRO_TAG (default repro)/bench_<w>.json
 set -u
-ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd $ROOT
-O=$ROOT/gpurun_out/r04final; mkdir -p $O
+O=$ROOT/gpurun_out/${REPRO_TAG:-repro}; mkdir -p $O
 for w in ${WORKLOADS:-sw_local nw_tb semi pairhmm sw_local_300 sw_local_start sw_local_tb semi_start semi_banded nvbio_gotoh nvbio_banded ksw nw_score cpu_plumbing}; do
   timeout -k 10 400 python3 bench.py --workload $w > $O/bench_$w.json 2> $O/bench_$w.err
   rc=$?
