@@ -781,7 +781,12 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? kW16_TB_WAVES
             step_global_tb<R, true>(T, top ? dtop : hd, top ? NN : fu, xs, Hin, Hout, Ek, dw, fdummy, KX, OEX, NN, j);
             ++c;
         };
+        // columns past ymaxw (the wave's widest padded target; the walk starts at most at column
+        // tl <= ymaxw, Q9) are never visited: a lane whose window runs past them stops there
+        // (the table reads of those columns fell outside the slot's staged positions)
+        const uint32_t tmax = (uint32_t)L <= ymaxw ? min(WD, (ymaxw + 1u - (uint32_t)L + 3u) & ~3u) : 0u;
         for (uint32_t t = 0; t < WD; t += 4) {
+            if (t >= tmax) break;                                    // (lane-divergent: no DPP in the band pass)
             const uint4 B2a = sp[t / 2 + 4], B2b = sp[t / 2 + 5];   // entries t + 8 .. t + 11
             bstep(0, HA, HB, B0a.x, B0a.w);
             bstep(1, HB, HA, B0a.z, B0b.y);

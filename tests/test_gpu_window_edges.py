@@ -224,6 +224,14 @@ def test_global_traceback_short_pairs_every_band(engine, monkeypatch):
         monkeypatch.setenv("GASALX_TB_BAND_W", w)
         assert "_tbband_" in plan(kw, 40, 40)
         check(engine, b, kw, cigar=True)
+    # queries much longer than their targets (lanes whose band window lies past the
+    # wave's widest target stop at it), the long queries' rows beyond the targets in most lanes
+    qs, ts = helpers.random_pairs(rng, 1500, 200, 300, 1, 60)
+    b = G.Batch.from_pairs(qs, ts)
+    for w in ("2", "10"):
+        monkeypatch.setenv("GASALX_TB_BAND_W", w)
+        assert "_tbband_" in plan(kw, 300, 60)
+        check(engine, b, kw, cigar=True)
 
 
 # ---------------------------------------------------------- SEMI-GLOBAL ----
