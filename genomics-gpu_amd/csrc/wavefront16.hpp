@@ -1038,8 +1038,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? kW16_TB_WAVES
                 const pk_u2 below = __builtin_elementwise_min(__builtin_elementwise_sub_sat(GX_AS(pk_u2, thr),
                                                                                             GX_AS(pk_u2, key[k])), one);
                 const uint32_t col = GX_AS(uint32_t, GX_AS(pk_u2, cb) - GX_AS(pk_u2, t));
-                const uint32_t code = (((col & 0xFFF8FFF8u) << 5) | (col & 0x00070007u) | ((uint32_t)(k << 3) * 0x10001u)) |
-                                      GX_AS(uint32_t, below * ffff);
+                // (a 16-bit shift per half: the masked rows' col is garbage, and a 32-bit shift would
+                // carry its high bits into the other half's code)
+                const pk_u2 sh5 = {5, 5};
+                const uint32_t code = GX_AS(uint32_t, GX_AS(pk_u2, col & 0xFFF8FFF8u) << sh5) | (col & 0x00070007u) |
+                                      ((uint32_t)(k << 3) * 0x10001u) | GX_AS(uint32_t, below * ffff);
                 bc = GX_AS(uint32_t, __builtin_elementwise_min(GX_AS(pk_u2, bc), GX_AS(pk_u2, code)));
             }
 #pragma unroll
