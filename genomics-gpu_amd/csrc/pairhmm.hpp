@@ -63,38 +63,24 @@ __global__ __launch_bounds__(256, kHmmWaves) void pairhmm_kernel(HmmArgs A) {
     uint32_t R = 0, H = 0, ro = 0, ho = 0;
     if (valid) { R = A.rlen[pair]; H = A.hlen[pair]; ro = A.roff[pair]; ho = A.hoff[pair]; }
 
-    // stage haplotypes; note whether the block holds a base other than A/C/G/T.  Every global load
-    // of the prologue is issued before any is used: in per-byte / per-row conditionals they
-    // compiled to one load + s_waitcnt vmcnt(0) each, ~24 serialised memory latencies per wave,
-    // and the waves of a launch round start together, so the SIMDs idled through them
+    // stage haplotypes; note whether the block holds a base other than A/C/G/T
     const uint32_t stride = A.lds_stride;
     uint8_t *wl = lds + (size_t)wave * P * stride;
     const uint32_t words = stride >> 2;
     bool other = false;
-    constexpr int CH = 8;                                    // staging rounds in flight together
-    for (uint32_t base0 = 0; base0 < P * words; base0 += 64 * CH) {
-        uint32_t hb[CH][4];
-#pragma unroll
-        for (int it = 0; it < CH; ++it) {
-            const uint32_t idx = base0 + it * 64 + lane;
-            const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
-            const uint32_t pH = __shfl(H, ps * G), pho = __shfl(ho, ps * G);
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                hb[it][b] = idx < P * words && 4 * w + b < pH ? (uint32_t)A.haps[pho + 4 * w + b] : 0x100u;
-        }
-#pragma unroll
-        for (int it = 0; it < CH; ++it) {
-            const uint32_t idx = base0 + it * 64 + lane;
-            const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
+    for (uint32_t base = 0; base < P * words; base += 64) {
+        const uint32_t idx = base + lane;
+        const uint32_t ps = min(idx / words, (uint32_t)P - 1), w = idx - ps * words;
+        const uint32_t pH = __shfl(H, ps * G), pho = __shfl(ho, ps * G);
+        if (idx < P * words) {
             uint32_t v = 0;
-#pragma unroll
             for (int b = 0; b < 4; ++b)
-                if (hb[it][b] != 0x100u) {
-                    other |= !acgt(hb[it][b]);
-                    v |= hb[it][b] << (8 * b);
+                if (4 * w + b < pH) {
+                    const uint32_t hb = A.haps[pho + 4 * w + b];
+                    other |= !acgt(hb);
+                    v |= hb << (8 * b);
                 }
-            if (idx < P * words) reinterpret_cast<uint32_t *>(wl + ps * stride)[w] = v;
+            reinterpret_cast<uint32_t *>(wl + ps * stride)[w] = v;
         }
     }
     const uint8_t *hap = wl + slot * stride;
@@ -113,44 +99,23 @@ __global__ __launch_bounds__(256, kHmmWaves) void pairhmm_kernel(HmmArgs A) {
     typedef float hmf2 __attribute__((ext_vector_type(2)));
     hmf2 deal[RR];
     const float D0 = valid && H ? __fdiv_rn(c0, (float)H) : 0.f;      // constant[0]/(float)H
-    // the rows' parameters: every load first (QUALS: the quality bytes, then the ph2pr entries)
-    float q_[RR], d_[RR], x_[RR], a_[RR];
-    uint32_t rb_[RR];
 #pragma unroll
     for (int k = 0; k < RR; ++k) {
         const int32_t i = r0 + k;
         const bool in = valid && i >= 0;
-        rb_[k] = in ? A.reads[ro + i] : 0x100u;
-        if (QUALS) {
-            // (indices only here; the table reads follow once every byte is in)
-            q_[k] = __int_as_float(in ? (int32_t)(A.bq[ro + i] & 127u) : 0);
-            d_[k] = __int_as_float(in ? (int32_t)(A.iq[ro + i] & 127u) : 0);
-            x_[k] = __int_as_float(in ? (int32_t)(A.dq[ro + i] & 127u) : 0);
-        } else {
-            q_[k] = in ? A.qm[ro + i] : 0.f;
-            d_[k] = in ? A.delta[ro + i] : 0.f;
-            x_[k] = in ? A.xiksi[ro + i] : 0.f;
-            a_[k] = in ? A.alpha[ro + i] : 0.f;
+        float q = 0.f, d = 0.f, x = 0.f, a = 0.f;
+        if (in) {
+            if (QUALS) {
+                const uint32_t b = A.bq[ro + i] & 127u, iqv = A.iq[ro + i] & 127u, dqv = A.dq[ro + i] & 127u;
+                q = A.ph2pr[b];
+                d = A.ph2pr[iqv];
+                x = A.ph2pr[dqv];
+                a = __fsub_rn(1.0f, A.ph2pr[(iqv + dqv) & 127u]);
+            } else {
+                q = A.qm[ro + i]; d = A.delta[ro + i]; x = A.xiksi[ro + i]; a = A.alpha[ro + i];
+            }
         }
-    }
-    if (QUALS) {
-#pragma unroll
-        for (int k = 0; k < RR; ++k) {
-            const bool in = valid && r0 + k >= 0;
-            const uint32_t b = (uint32_t)__float_as_int(q_[k]), iqv = (uint32_t)__float_as_int(d_[k]),
-                           dqv = (uint32_t)__float_as_int(x_[k]);
-            q_[k] = in ? A.ph2pr[b] : 0.f;
-            d_[k] = in ? A.ph2pr[iqv] : 0.f;
-            x_[k] = in ? A.ph2pr[dqv] : 0.f;
-            a_[k] = in ? __fsub_rn(1.0f, A.ph2pr[(iqv + dqv) & 127u]) : 0.f;
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < RR; ++k) {
-        const int32_t i = r0 + k;
-        const bool in = valid && i >= 0;
-        const float q = q_[k], d = d_[k], x = x_[k], a = a_[k];
-        rb[k] = rb_[k];
+        rb[k] = in ? A.reads[ro + i] : 0x100u;
         other |= in && !acgt(rb[k]);
         qm1[k] = in ? __fsub_rn(1.0f, q) : 0.f;     // Qm_1 = constant[1] - Qm
         qm3[k] = in ? __fdiv_rn(q, 3.0f) : 0.f;     // fdividef(Qm, 3) (<= 2 ulp in the reference)

@@ -606,74 +606,38 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? kW16_TB_WAVES
     const uint32_t words = A.lds_stride >> 3;            // positions per slot, >= ymaxw + 2G + 4, multiple of 4
     uint2 *wl = reinterpret_cast<uint2 *>(lds) + (size_t)wave * S * words;
     bool other = false;                                  // a code the packed path cannot score
-    // Every global load of the prologue is issued before any is used: loads inside per-row or
-    // per-quad conditionals compiled to one load + s_waitcnt vmcnt(0) each, i.e. ~50 serialised
-    // memory latencies per wave before its sweep (config 2: R = 19 rows x 2 pairs, 6 staging
-    // rounds x 2).  (The loads stay predicated -- a batch of empty sequences has no bytes to read --
-    // but nothing reads their values before the last one is issued.)
-    constexpr int CH = 8;                                // staging rounds whose loads are in flight together
-    const uint32_t quads = S * (words >> 2);
-    for (uint32_t base0 = 0; base0 < quads; base0 += 64 * CH) {
-        uint32_t v[CH][2], yl_[CH][2];
-        bool in_[CH][2];
+    for (uint32_t base = 0; base < S * (words >> 2); base += 64) {
+        const uint32_t idx = base + lane;
+        const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
+        const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;   // first position of this quad
+        uint32_t tab[2][4];
 #pragma unroll
-        for (int it = 0; it < CH; ++it) {
-            const uint32_t idx = base0 + it * 64 + lane;
-            const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
-            const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;   // first position of this quad
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
+            const uint32_t ylen = __shfl(yl[h], ps * G);
+            uint32_t v = 0;
+            const bool in = (int32_t)y0 >= 0 && y0 < yp;
+            if (in) v = load4_codes_dir(A, Y, yof, ylen, y0 >> 2);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t yp = __shfl(ypad[h], ps * G), yof = __shfl(yo[h], ps * G);
-                yl_[it][h] = __shfl(yl[h], ps * G);
-                in_[it][h] = (int32_t)y0 >= 0 && y0 < yp && idx < quads;
-                v[it][h] = in_[it][h] ? load4_codes_dir(A, Y, yof, yl_[it][h], y0 >> 2) : 0u;
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t l = in ? letter_of((v >> (8 * j)) & 15u, A.nval) : 6u;
+                other |= l == 5;
+                // traceback reads the first pad query row, scored here as -K: exact for
+                // pad x base columns, not for pad x real-N columns (N == N is a match)
+                if (GT && !A.has_npen) other |= l == 4 && y0 + j < ylen;
+                if (GT) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
+                tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
             }
         }
+        if (idx < S * (words >> 2)) {
+            uint2 *dst = wl + ps * words + 4 * (idx - ps * (words >> 2));
 #pragma unroll
-        for (int it = 0; it < CH; ++it) {
-            const uint32_t idx = base0 + it * 64 + lane;
-            const uint32_t ps = min(idx / (words >> 2), (uint32_t)S - 1);
-            const uint32_t y0 = 4 * (idx - ps * (words >> 2)) - G;
-            uint32_t tab[2][4];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const bool in = in_[it][h];
-                const uint32_t ylen = yl_[it][h];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t l = in ? letter_of((v[it][h] >> (8 * j)) & 15u, A.nval) : 6u;
-                    other |= l == 5;
-                    // traceback reads the first pad query row, scored here as -K: exact for
-                    // pad x base columns, not for pad x real-N columns (N == N is a match)
-                    if (GT && !A.has_npen) other |= l == 4 && y0 + j < ylen;
-                    if (GT) other |= in && y0 + j >= ylen && l != 4;   // start-cell fix assumes N pads
-                    tab[h][j] = l == 6 ? t_out : l == 4 ? t_n : (t_mis & ~(0xFFu << (8 * l))) | (t_match << (8 * l));
-                }
-            }
-            if (idx < quads) {
-                uint2 *dst = wl + ps * words + 4 * (idx - ps * (words >> 2));
-#pragma unroll
-                for (int j = 0; j < 4; ++j) dst[j] = make_uint2(tab[0][j], tab[1][j]);
-            }
+            for (int j = 0; j < 4; ++j) dst[j] = make_uint2(tab[0][j], tab[1][j]);
         }
     }
     // ---- register-axis letters: selector bytes 0 / 2 (0x0C = constant 0 outside) ----
     const uint32_t r0 = lg * R;
     uint32_t xs[R];
-    uint32_t xb[2][R];                                   // the rows' bytes (or packed words), loaded first
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-        const uint32_t r = r0 + k;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            // (WITH_START reverse pass: position r of "the first xl bases, reversed", N past xl)
-            const bool ld = valid[h] && r < xpad[h] && !(A.rev && r >= xl[h]);
-            const uint32_t pos = A.rev ? xl[h] - 1u - r : r;
-            xb[h][k] = !ld ? 0u
-                       : A.packed ? reinterpret_cast<const uint32_t *>(X)[(xo[h] >> 3) + (pos >> 3)]
-                                  : (uint32_t)X[xo[h] + pos];
-        }
-    }
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t r = r0 + k;
@@ -681,10 +645,11 @@ __global__ __launch_bounds__(kBlock, ALGO_ == WF16_GLOBAL_TB ? kW16_TB_WAVES
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (valid[h] && r < xpad[h]) {
+                // (WITH_START reverse pass: position r of "the first xl bases, reversed", N past xl)
                 const uint32_t pos = A.rev ? xl[h] - 1u - r : r;
                 const uint32_t cde = A.rev && r >= xl[h] ? (uint32_t)A.nval
-                                     : A.packed ? (xb[h][k] >> (28 - 4 * (pos & 7))) & 15u
-                                                : xb[h][k] & 15u;
+                                     : A.packed ? (load4_codes(X, xo[h], pos >> 2, 1) >> (8 * (pos & 3))) & 15u
+                                                : (uint32_t)X[xo[h] + pos] & 15u;
                 const uint32_t l = letter_of(cde, A.nval);
                 if (r < xl[h]) {
                     other |= l >= 4;                 // real positions must be A/C/G/T

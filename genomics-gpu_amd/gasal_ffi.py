@@ -119,7 +119,9 @@ def lib():
         _lib = ctypes.CDLL(LIB_PATH)
         _lib.gasalx_last_error.restype = ctypes.c_char_p
         for name in EXPORTS:
-            if name != "gasalx_last_error":
+            # (an older build loaded through GASALX_LIB for an A/B run may lack the newest entry
+            # points; tests/test_capi.py checks the default build exports every one)
+            if name != "gasalx_last_error" and hasattr(_lib, name):
                 getattr(_lib, name).restype = ctypes.c_int
     return _lib
 
