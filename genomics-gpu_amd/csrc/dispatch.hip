@@ -498,6 +498,13 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
                               : wf16_lookup(pl.wf_algo, pl.tb, pl.G16, pl.R16, pl.key2, A.stop != nullptr, pl.ku16,
                                             A.lstop != nullptr && pl.kf16 != 0 && !pl.kseg_shift, pl.kseg_shift != 0,
                                             pl.tb && pl.kf16 != 0);
+        // WITH_START reverse passes: the register axis sized per block (rclass.hip)
+        const bool lrs = pl.wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && A.lstop != nullptr && pl.kf16 != 0 &&
+                         !pl.kseg_shift;
+        if (A.rev && !pl.tb_band && (A.stop != nullptr || lrs) && env_flag("GASALX_RCLASS", true)) {
+            const int ra = A.stop ? WF16_SEMI_STOP : pl.ku16 ? WF16_LOCAL_U16_RS : WF16_LOCAL_RS;
+            if (WfFn rc = wf16_rclass_lookup(ra, pl.G16, pl.R16)) f16 = rc;
+        }
         if (pl.kseg_shift) {
             // the finished segments' keys per wave: saves at steps M, 2M, ... < nsteps <= C + G - 1
             const uint32_t nsave = std::max<uint32_t>(1u, (pl.kf16 + (uint32_t)pl.G16 - 2u) >> pl.kseg_shift);
@@ -619,25 +626,30 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
                          int packed, const gasalx_batch &b, const BatchShape &shape, const int32_t *score,
                          const int32_t *qend, const int32_t *tend, int32_t *qstart, int32_t *tstart, hipStream_t st) {
     const uint32_t n = b.n_alns;
-    const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t), t8w = t8 / 8;
-    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 6 + (size_t)(t8w + 1) * 8 + 64));
+    const uint32_t q8 = pad8(shape.max_q), t8 = pad8(shape.max_t), t8w = t8 / 8, q8w = q8 / 8;
+    // LOCAL: slots that stop early (the drift sweep's lstop) share waves (start.hpp rev_bucket),
+    // and the query words come first when the two-key histogram fits LDS
+    const bool lstop = mode == REV_LOCAL;
+    const bool qkey = lstop && (size_t)(q8w + 1) * (t8w + 1) * 8 <= 64 * 1024;
+    const uint32_t nb = qkey ? (q8w + 1) * (t8w + 1) : t8w + 1;
+    HIPCHK(ws.rev_meta.reserve((size_t)n * 4 * 6 + (size_t)nb * 8 + 64));
     uint32_t *meta = ws.rev_meta.as<uint32_t>();
     uint32_t *rqlen = meta, *rtlen = meta + n;
     int32_t *rscore = reinterpret_cast<int32_t *>(meta + 2 * (size_t)n);
     int32_t *rqend = rscore + n, *rtend = rscore + 2 * (size_t)n;
     uint32_t *perm = meta + 5 * (size_t)n;
-    uint32_t *hist = meta + 6 * (size_t)n, *cursor = hist + t8w + 1;
+    uint32_t *hist = meta + 6 * (size_t)n, *cursor = hist + nb;
     // counting sort of the pairs by reversed target words (longest first)
-    const size_t sh = (size_t)(t8w + 1) * 4;
+    const size_t sh = (size_t)nb * 4;
     if (2 * sh > 64 * 1024) { set_error("WITH_START: target too long for the slot sort"); return GASALX_ERANGE; }
     HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-    // LOCAL: slots that stop early (the drift sweep's lstop) share waves (start.hpp rev_bucket)
-    const bool lstop = mode == REV_LOCAL;
     const int32_t *skey = lstop ? score : nullptr;
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match);
-    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
+    const uint32_t *kql = qkey ? b.q_lens : nullptr;
+    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match, kql, qend,
+                                                       q8w, nb);
+    rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nb);
     rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm, nullptr,
-                                                              skey, p.match);
+                                                              skey, p.match, kql, qend, q8w, nb);
     rev_len_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, q, b.q_offsets, b.q_lens, b.t_lens, qend, tend, packed,
                                                       (uint32_t)(p.n_code & 0xF), n, rqlen, rtlen);
     HIPCHK(hipGetLastError());

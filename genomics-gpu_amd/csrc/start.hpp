@@ -55,6 +55,8 @@
 // The reverse pass's slots are sorted by reversed target words, longest first
 // (counting sort, perm: slot -> pair): a wave's step count is set by its longest
 // target, and unrelated pairs end early, so their reversed rectangles are short.
+// LOCAL sorts by the reversed query's words first: the class kernels of rclass.hip run
+// each block with the rows its longest query needs.
 // Lengths and results of the reverse pass are per pair.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -93,16 +95,23 @@ __device__ __forceinline__ uint32_t seq_byte(const uint8_t *seq, uint32_t off, u
 // sort key of the reverse pass's slots: the reversed target length, or (LOCAL with the forward
 // scores, whose sweep stops once the score is reached) the shorter of it and a span estimate of
 // the alignment, 2 * ceil(score / match) + 16 columns -- a wave's step count is set by its
-// slowest pair, so pairs that will stop early share waves (a heuristic: the results do not
-// depend on the order)
+// slowest pair, so pairs that will stop early share waves.  LOCAL with qlen: first by the
+// reversed query's words (the register axis, which rclass.hip sizes per block), then by that.
+// (A heuristic: the results do not depend on the order.)  Buckets: (q8w + 1) x (t8w + 1) with
+// qlen, t8w + 1 without; 0 = longest.
 __device__ __forceinline__ uint32_t rev_bucket(int32_t mode, const uint32_t *tlen, const int32_t *tend, uint32_t k,
-                                               uint32_t t8w, const int32_t *score = nullptr, int32_t a = 1) {
+                                               uint32_t t8w, const int32_t *score = nullptr, int32_t a = 1,
+                                               const uint32_t *qlen = nullptr, const int32_t *qend = nullptr,
+                                               uint32_t q8w = 0) {
     uint32_t L = rev_tlen(mode, tlen, tend, k);
     if (score && mode == REV_LOCAL && a > 0) {
         const int32_t sc = max(score[k], 0);
         L = min(L, (uint32_t)(2 * ((sc + a - 1) / a) + 16));
     }
-    return t8w - min((L + 7) >> 3, t8w);   // 0 = longest
+    const uint32_t b = t8w - min((L + 7) >> 3, t8w);
+    if (!qlen || mode != REV_LOCAL) return b;
+    const uint32_t qb = q8w - min(start_regs(qlen[k], qend[k]), q8w);
+    return qb * (t8w + 1) + b;
 }
 
 // cnt[b] += the number of active lanes of the wave with bucket b, one LDS atomic per distinct
@@ -127,16 +136,20 @@ __device__ __forceinline__ uint32_t wave_bucket_add(uint32_t *cnt, uint32_t b, b
     return pos;
 }
 
+// nb: the bucket count (rev_bucket)
 __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                        uint32_t n, uint32_t t8w, uint32_t *hist,
-                                                       const int32_t *score = nullptr, int32_t a = 1) {
-    extern __shared__ uint32_t cnt[];   // t8w + 1 buckets
-    for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
+                                                       const int32_t *score = nullptr, int32_t a = 1,
+                                                       const uint32_t *qlen = nullptr, const int32_t *qend = nullptr,
+                                                       uint32_t q8w = 0, uint32_t nb = 0) {
+    extern __shared__ uint32_t cnt[];   // nb buckets
+    if (!nb) nb = t8w + 1;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a) : 0u, k < n);
+    (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u, k < n);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
         if (cnt[i]) atomicAdd(&hist[i], cnt[i]);
 }
 
@@ -160,16 +173,20 @@ __global__ __launch_bounds__(256) void rev_scan_kernel(const uint32_t *hist, uin
 __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                           uint32_t n, uint32_t t8w, uint32_t *cursor,
                                                           uint32_t *perm, uint32_t *inv = nullptr,
-                                                          const int32_t *score = nullptr, int32_t a = 1) {
-    extern __shared__ uint32_t cnt[];   // [t8w+1] counts, then [t8w+1] bases
-    uint32_t *base = cnt + t8w + 1;
-    for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x) cnt[i] = 0;
+                                                          const int32_t *score = nullptr, int32_t a = 1,
+                                                          const uint32_t *qlen = nullptr,
+                                                          const int32_t *qend = nullptr, uint32_t q8w = 0,
+                                                          uint32_t nb = 0) {
+    extern __shared__ uint32_t cnt[];   // [nb] counts, then [nb] bases
+    if (!nb) nb = t8w + 1;
+    uint32_t *base = cnt + nb;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a) : 0u;
+    const uint32_t b = k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u;
     const uint32_t local = wave_bucket_add(cnt, b, k < n);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i <= t8w; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
         if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
     __syncthreads();
     if (k < n) {
