@@ -501,7 +501,7 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         // WITH_START reverse passes: the register axis sized per block (rclass.hip)
         const bool lrs = pl.wf_algo == WF_LOCAL && !pl.tb && !pl.key2 && A.lstop != nullptr && pl.kf16 != 0 &&
                          !pl.kseg_shift;
-        if (A.rev && !pl.tb_band && (A.stop != nullptr || lrs) && env_flag("GASALX_RCLASS", true)) {
+        if (A.rev && !pl.tb_band && (A.stop != nullptr || lrs)) {
             const int ra = A.stop ? WF16_SEMI_STOP : pl.ku16 ? WF16_LOCAL_U16_RS : WF16_LOCAL_RS;
             if (WfFn rc = wf16_rclass_lookup(ra, pl.G16, pl.R16)) f16 = rc;
         }
