@@ -559,7 +559,7 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     } else {
         // the class sizes, read back: one synchronisation of the stream (gasalx.h, max_t_len)
         HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-        rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, hist);
+        rev_hist_kernel<<<sort_grid(n), 256, sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, hist);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(h.data(), hist, sh, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -569,7 +569,7 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     A.perm = nullptr;
     if (classes > 1) {                                       // counting sort: longest targets first
         rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, t8w + 1);
-        rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, cursor, perm);
+        rev_scatter_kernel<<<sort_grid(n), 256, 2 * sh, st>>>(REV_PLAIN, A.tlen, nullptr, n, t8w, cursor, perm);
         HIPCHK(hipGetLastError());
         A.perm = perm;
     }
@@ -645,10 +645,10 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     HIPCHK(hipMemsetAsync(hist, 0, sh, st));
     const int32_t *skey = lstop ? score : nullptr;
     const uint32_t *kql = qkey ? b.q_lens : nullptr;
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match, kql, qend,
+    rev_hist_kernel<<<sort_grid(n), 256, sh, st>>>(mode, b.t_lens, tend, n, t8w, hist, skey, p.match, kql, qend,
                                                        q8w, nb);
     rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nb);
-    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm, nullptr,
+    rev_scatter_kernel<<<sort_grid(n), 256, 2 * sh, st>>>(mode, b.t_lens, tend, n, t8w, cursor, perm, nullptr,
                                                               skey, p.match, kql, qend, q8w, nb);
     rev_len_kernel<<<grid_for(n, 256), 256, 0, st>>>(mode, q, b.q_offsets, b.q_lens, b.t_lens, qend, tend, packed,
                                                       (uint32_t)(p.n_code & 0xF), n, rqlen, rtlen);
@@ -699,9 +699,9 @@ static int geometry_perm(Workspace &ws, const gasalx_batch &b, const BatchShape 
     uint32_t *perm = ws.sort_meta.as<uint32_t>(), *klen = perm + n, *hist = klen + n, *cursor = hist + nkeys + 1;
     band16_key_kernel<<<grid_for(n, 256), 256, 0, st>>>(b.q_lens, b.t_lens, n, trw, klen);
     HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-    rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, hist);
+    rev_hist_kernel<<<sort_grid(n), 256, sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, hist);
     rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, nkeys + 1);
-    rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, cursor, perm);
+    rev_scatter_kernel<<<sort_grid(n), 256, 2 * sh, st>>>(REV_PLAIN, klen, nullptr, n, nkeys, cursor, perm);
     HIPCHK(hipGetLastError());
     *perm_out = perm;
     return GASALX_OK;
@@ -845,9 +845,9 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
                 HIPCHK(ws.sort_meta.reserve((size_t)n * 8 + (size_t)(s8w + 1) * 8 + 64));
                 uint32_t *perm = ws.sort_meta.as<uint32_t>(), *inv = perm + n, *hist = inv + n, *cursor = hist + s8w + 1;
                 HIPCHK(hipMemsetAsync(hist, 0, sh, st));
-                rev_hist_kernel<<<grid_for(n, 256), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
+                rev_hist_kernel<<<sort_grid(n), 256, sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w, hist);
                 rev_scan_kernel<<<1, 256, 0, st>>>(hist, cursor, s8w + 1);
-                rev_scatter_kernel<<<grid_for(n, 256), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w,
+                rev_scatter_kernel<<<sort_grid(n), 256, 2 * sh, st>>>(REV_PLAIN, slen, nullptr, n, s8w,
                                                                           cursor, perm, inv);
                 HIPCHK(hipGetLastError());
                 A.perm = perm;

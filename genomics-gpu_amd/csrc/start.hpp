@@ -62,6 +62,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 namespace gx {
 
 enum RevMode { REV_LOCAL = 0, REV_SEMI = 1, REV_PLAIN = 2 };   // PLAIN: sort by the lengths given
@@ -136,7 +138,12 @@ __device__ __forceinline__ uint32_t wave_bucket_add(uint32_t *cnt, uint32_t b, b
     return pos;
 }
 
-// nb: the bucket count (rev_bucket)
+// The sort kernels walk the pairs grid-stride (sort_grid: at most 1,024 blocks) and add a
+// block's counts to the global ones once: one global atomic per bucket and block of 256 pairs
+// serialised on the batch's few buckets (0.45 ms per 10 M config-4 pairs, 0.08 ms per 1 M
+// config-2 pairs).  nb: the bucket count (rev_bucket).
+inline int sort_grid(uint32_t n) { return (int)std::min<uint32_t>((n + 255) / 256, 1024u); }
+
 __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint32_t *tlen, const int32_t *tend,
                                                        uint32_t n, uint32_t t8w, uint32_t *hist,
                                                        const int32_t *score = nullptr, int32_t a = 1,
@@ -146,8 +153,10 @@ __global__ __launch_bounds__(256) void rev_hist_kernel(int32_t mode, const uint3
     if (!nb) nb = t8w + 1;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u, k < n);
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {   // wave-uniform trips
+        const uint32_t k = base + threadIdx.x;
+        (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u, k < n);
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
         if (cnt[i]) atomicAdd(&hist[i], cnt[i]);
@@ -182,16 +191,26 @@ __global__ __launch_bounds__(256) void rev_scatter_kernel(int32_t mode, const ui
     uint32_t *base = cnt + nb;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t b = k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u;
-    const uint32_t local = wave_bucket_add(cnt, b, k < n);
+    // the block's counts over all its pairs, one global reservation per bucket, then the positions
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
+        const uint32_t k = b0 + threadIdx.x;
+        (void)wave_bucket_add(cnt, k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u, k < n);
+    }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x)
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
         if (cnt[i]) base[i] = atomicAdd(&cursor[i], cnt[i]);
+        cnt[i] = 0;
+    }
     __syncthreads();
-    if (k < n) {
-        perm[base[b] + local] = k;
-        if (inv) inv[k] = base[b] + local;
+    for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
+        const uint32_t k = b0 + threadIdx.x;
+        const uint32_t b = k < n ? rev_bucket(mode, tlen, tend, k, t8w, score, a, qlen, qend, q8w) : 0u;
+        const uint32_t local = wave_bucket_add(cnt, b, k < n);
+        if (k < n) {
+            perm[base[b] + local] = k;
+            if (inv) inv[k] = base[b] + local;
+        }
     }
 }
 

@@ -463,17 +463,32 @@ __device__ __forceinline__ void wf_block(const WfArgs &A, uint8_t *lds, const ui
         wf_body<ALGO, KEYS, TB, G, R, false, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
 }
 
-// As the fallback of a packed launch (A.skip) the grid is capped (dispatch.hip wf_fallback_grid)
-// and each block walks the virtual blocks bx, bx + gridDim.x, ...: a batch the packed kernel took
-// whole then costs a few thousand flag reads instead of a full grid of early exits (25 us per
-// 1 M config-2 pairs).  Each wave stages into its own LDS region, so consecutive virtual blocks
-// need no barrier between them beyond those of the body (block-uniform loop).
+// As the fallback of a packed launch (A.skip) the grid is capped (dispatch.hip wf_grid) and each
+// block walks the virtual blocks bx, bx + gridDim.x, ...: a batch the packed kernel took whole
+// then costs a few flag reads per block instead of a full grid of early exits.  The flags of 64
+// of its virtual blocks are read at once, one per lane, and only those holding a declined pair
+// are run (one flag read per virtual block in turn cost 32 us per 1 M config-2 pairs and 0.44 ms
+// per 10 M config-4 pairs: a chain of dependent loads).  Every wave reads the same flags, so the
+// loop is block-uniform; each wave stages into its own LDS region, so consecutive virtual blocks
+// need no barrier between them beyond those of the body.
 template <int ALGO, bool KEYS, bool TB, int G, int R, bool STOP = false>
 __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     constexpr uint32_t PPB = kWavesPerBlock * (64 / G);
     const uint32_t nblk = (A.n + PPB - 1) / PPB;
-    for (uint32_t bx = blockIdx.x; bx < nblk; bx += gridDim.x) wf_block<ALGO, KEYS, TB, G, R, STOP>(A, lds, bx);
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x; base < nblk; base += 64 * gridDim.x) {
+        const uint32_t bx = base + lane * gridDim.x;
+        bool run = bx < nblk;
+        if (run && A.skip) {   // a declined pair: some flag over its slots is clear
+            const uint32_t f0 = bx * PPB / A.skip_ppb, f1 = (min(bx * PPB + PPB, A.n) - 1) / A.skip_ppb;
+            bool all = true;
+            for (uint32_t f = f0; f <= f1; ++f) all &= A.skip[f] != 0;
+            run = !all;
+        }
+        for (uint64_t m = __ballot(run); m; m &= m - 1)
+            wf_block<ALGO, KEYS, TB, G, R, STOP>(A, lds, base + (uint32_t)__builtin_ctzll(m) * gridDim.x);
+    }
 }
 
 }  // namespace gx
