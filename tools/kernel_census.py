@@ -23,15 +23,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def code_object(lib, tmp):
+def code_objects(lib, tmp):
+    """The gfx950 code objects of the library: its .hip_fatbin section holds one offload bundle per
+    HIP translation unit (dispatch.hip, local_rs.hip, rclass.hip, ...), each unbundled apart."""
     fat = os.path.join(tmp, "fat.bin")
-    subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, lib], check=True,
-                   capture_output=True)
-    co = os.path.join(tmp, "k.co")
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + fat,
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True,
-                   capture_output=True)
-    return co
+    # an explicit output file: with the input alone llvm-objcopy rewrites the library in place,
+    # which changed its sha256 (and so unmatched the PMC summaries that record it)
+    subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section=.hip_fatbin=" + fat, lib, os.path.join(tmp, "copy.so")],
+                   check=True, capture_output=True)
+    data = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [i for i in range(len(data)) if data.startswith(magic, i)] if len(data) < (1 << 28) else [0]
+    cos = []
+    for k, a in enumerate(starts):
+        b = starts[k + 1] if k + 1 < len(starts) else len(data)
+        part = os.path.join(tmp, f"fat{k}.bin")
+        open(part, "wb").write(data[a:b])
+        co = os.path.join(tmp, f"k{k}.co")
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", "--input=" + part,
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], capture_output=True)
+        if r.returncode == 0 and os.path.getsize(co) > 0:
+            cos.append(co)
+    return cos
+
+
+def code_object(lib, tmp, sym=None):
+    """The code object holding kernel `sym` (mangled), or the first one."""
+    cos = code_objects(lib, tmp)
+    if sym is not None:
+        for co in cos:
+            out = subprocess.run([f"{LLVM}/llvm-objdump", "-t", co], check=True, capture_output=True, text=True).stdout
+            if any(ln.split()[-1] == sym for ln in out.splitlines() if ln.split()):
+                return co
+    return cos[0]
 
 
 def disasm(co, sym):
@@ -74,8 +98,9 @@ def price(op, text, table):
 def mangled(lib, name):
     """The code object's kernel symbol whose demangled form is `name` (as rocprofv3 prints it)."""
     with tempfile.TemporaryDirectory() as tmp:
-        co = lib if lib.endswith(".co") else code_object(lib, tmp)
-        out = subprocess.run([f"{LLVM}/llvm-objdump", "-t", co], check=True, capture_output=True, text=True).stdout
+        out = ""
+        for co in ([lib] if lib.endswith(".co") else code_objects(lib, tmp)):
+            out += subprocess.run([f"{LLVM}/llvm-objdump", "-t", co], check=True, capture_output=True, text=True).stdout
     syms = sorted({ln.split()[-1] for ln in out.splitlines() if " F " in ln and ln.split()[-1].startswith("_Z")})
     dem = subprocess.run(["c++filt"], input="\n".join(syms), check=True, capture_output=True, text=True).stdout.split("\n")
     for m, d in zip(syms, dem):
@@ -87,7 +112,7 @@ def mangled(lib, name):
 def census(lib, sym, rates):
     table = rates_table(rates)
     with tempfile.TemporaryDirectory() as tmp:
-        ins = disasm(lib if lib.endswith(".co") else code_object(lib, tmp), sym)   # .co: a gfx950 code object
+        ins = disasm(lib if lib.endswith(".co") else code_object(lib, tmp, sym), sym)   # .co: a gfx950 code object
     addr = {a: i for i, (a, _, _) in enumerate(ins)}
     loops = []
     for i, (a, t, off) in enumerate(ins):
