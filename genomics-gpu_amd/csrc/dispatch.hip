@@ -389,7 +389,12 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             // band's half width w (window of lane lg: columns [max(lg*R - w, 0), + R + 2w))
             if (pl.packed16 && pl.tb && wf_algo == WF_GLOBAL && pl.R16 % 4 == 0 && env_flag("GASALX_TB_BAND", true)) {
                 const char *bw = std::getenv("GASALX_TB_BAND_W");
-                const int w = bw ? std::max(0, std::atoi(bw)) : 10;   // w 8-16 within 2 % (profiles/r04/k_nw_tb_w*.json)
+                // w = 22: config 3's paths stray up to 20 cells from the diagonal, and any pair
+                // that leaves its band costs the chain a full-matrix sweep and a second walk,
+                // latency floors however few pairs they hold; w = 10 -> 22 took config 3 from
+                // 2,953 to 3,647 GCUPS on one engine and 4,240 to 4,450-4,560 on three, though
+                // the band pass grows by 60 % (profiles/r05/n_band_width.md)
+                const int w = bw ? std::max(0, std::atoi(bw)) : 22;
                 pl.tb_band = true;
                 pl.band_w = (uint32_t)w;
                 pl.band_wd = ((uint32_t)(pl.R16 + 2 * w) + 3u) & ~3u;
