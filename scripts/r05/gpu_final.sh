@@ -5,7 +5,7 @@
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 cd $ROOT
-O=$ROOT/gpurun_out/r05final; mkdir -p $O
+O=$ROOT/gpurun_out/${FINAL_TAG:-r05final}; mkdir -p $O
 fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
 step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
