@@ -10,6 +10,7 @@
 
 #include "engine.hpp"
 #include "nvbio.hpp"
+#include "nvtrace.hpp"
 #include "nvbio16.hpp"
 #include "nvbanded.hpp"
 
@@ -308,6 +309,43 @@ int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t 
     }
     NvBandFn fn = al.aligner == NV_GOTOH ? nv_band_lookup_t<NV_GOTOH>(al.type, band) : nv_band_lookup_t<NV_SW>(al.type, band);
     hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+    return GASALX_OK;
+}
+
+
+// nvbio BatchedAlignmentTraceback (nvtrace.hpp): one pair per thread, flags and the previous row in
+// the caller's workspace (dir: max_p * max_t bytes per pair, row: 2 * (max_p + 1) int32 per pair)
+int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
+                        const gasalx_nv_strings &txt, uint32_t max_p, uint32_t max_t, uint8_t *dir, int32_t *row,
+                        int32_t *score, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
+                        uint32_t *n_ops, hipStream_t st) {
+    if (al.aligner != NV_GOTOH && al.aligner != NV_SW) {
+        set_error("traceback: Gotoh and Smith-Waterman aligners only");
+        return GASALX_EUNSUPPORTED;
+    }
+    if (al.type < 0 || al.type > 2) { set_error("bad alignment type"); return GASALX_EINVAL; }
+    for (uint32_t b : {pat.bits, txt.bits})
+        if (b != 2 && b != 4 && b != 8) { set_error("symbol bits must be 2, 4 or 8"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    if (!pat.words || !pat.offsets || !txt.words || !score || !src || !snk || !ops || !n_ops || !dir || !row) {
+        set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    NvTbArgs A;
+    A.pw = pat.words; A.poff = pat.offsets; A.pbits = pat.bits; A.pbig = pat.big_endian;
+    A.tw = txt.words; A.toff = txt.offsets; A.tlen0 = txt.offsets ? 0 : txt.length; A.tbits = txt.bits;
+    A.tbig = txt.big_endian;
+    A.match = al.match; A.mismatch = al.mismatch; A.go = al.gap_open; A.ge = al.gap_ext;
+    A.del = al.deletion; A.ins = al.insertion;
+    A.n = n; A.max_m = max_p; A.max_n = max_t;
+    A.dir = dir; A.row = row; A.score = score; A.src = src; A.snk = snk; A.ops = ops; A.ops_stride = ops_stride;
+    A.n_ops = n_ops;
+    using Fn = void (*)(NvTbArgs);
+    static const Fn tab[2][3] = {{&nv_traceback_kernel<false, 0>, &nv_traceback_kernel<false, 1>, &nv_traceback_kernel<false, 2>},
+                                 {&nv_traceback_kernel<true, 0>, &nv_traceback_kernel<true, 1>, &nv_traceback_kernel<true, 2>}};
+    hipLaunchKernelGGL(tab[al.aligner == NV_GOTOH ? 1 : 0][al.type], dim3((n + 255) / 256), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
     return GASALX_OK;

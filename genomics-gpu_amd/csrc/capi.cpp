@@ -37,13 +37,15 @@ struct gasalx_engine {
     gx::DevBuf h_reads, h_ro, h_rl, h_qm, h_de, h_xi, h_al, h_haps, h_ho, h_hl, h_res;
     gx::DevBuf h_bq, h_iq, h_dq, h_perm, ph2pr;   // PairHMM from qualities: staging + the ph2pr table
     gx::DevBuf nv_pw, nv_po, nv_tw, nv_to, nv_s, nv_s16;   // nvbio front-end staging
+    gx::DevBuf nv_dir, nv_row, nv_src, nv_snk, nv_ops, nv_nops;   // nvbio traceback: workspace + staging
     void release() {
         ws.release_all();
         for (HostSlot &s : slot) s.release();
         for (gx::DevBuf *b : {&q, &t, &qo, &to, &ql, &tl, &qop, &top, &seed, &o_score, &o_qe, &o_te, &o_qs, &o_ts,
                               &o_s2, &o_qe2, &o_te2, &o_cig, &o_nops, &lens_max, &h_reads, &h_ro, &h_rl, &h_qm,
                               &h_de, &h_xi, &h_al, &h_haps, &h_ho, &h_hl, &h_res, &h_bq, &h_iq, &h_dq, &h_perm,
-                              &ph2pr, &nv_pw, &nv_po, &nv_tw, &nv_to, &nv_s, &nv_s16})
+                              &ph2pr, &nv_pw, &nv_po, &nv_tw, &nv_to, &nv_s, &nv_s16, &nv_dir, &nv_row,
+                              &nv_src, &nv_snk, &nv_ops, &nv_nops})
             b->release();
     }
 };
@@ -637,6 +639,88 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al,
     rc = gx::nv_banded_score_device(*al, band, n, dp, dt, eng->nv_s.as<int32_t>(), st, max_span(pat->offsets, n));
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
+// nvbio BatchedAlignmentTraceback (nvtrace.hpp).  nvbio keeps its DP columns and checkpoints in
+// int16 (alignment/utils.h:49-64): the scores of every cell must stay within them.
+static int nv_tb_checks(const gasalx_nv_aligner *al, uint32_t max_p, uint32_t max_t, uint32_t ops_stride) {
+    const int64_t mag = std::max<int64_t>({std::abs((int64_t)al->match), std::abs((int64_t)al->mismatch),
+                                           std::abs((int64_t)al->gap_open), std::abs((int64_t)al->gap_ext),
+                                           std::abs((int64_t)al->deletion), std::abs((int64_t)al->insertion), 1});
+    if (((int64_t)max_p + max_t + 2) * mag > 32767) {
+        gx::set_error("traceback: scores would leave nvbio's int16 columns (lengths x |score|)");
+        return GASALX_ERANGE;
+    }
+    if (ops_stride < max_p + max_t) { gx::set_error("traceback: ops_stride < max pattern + max text length"); return GASALX_EINVAL; }
+    if ((uint64_t)max_p * max_t > (1ull << 24)) { gx::set_error("traceback: pattern x text above 16 M cells"); return GASALX_ERANGE; }
+    return GASALX_OK;
+}
+
+int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t n,
+                               const gasalx_nv_strings *pat, const gasalx_nv_strings *txt, uint32_t max_p,
+                               uint32_t max_t, int32_t *scores, uint32_t *sources, uint32_t *sinks, uint8_t *ops,
+                               uint32_t ops_stride, uint32_t *n_ops, void *stream) {
+    if (!eng || !al || !pat || !txt) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    if (!max_p || (txt->offsets && !max_t)) {   // read the offsets back (synchronises the stream)
+        std::vector<uint32_t> po(n + 1), to(txt->offsets ? n + 1 : 0);
+        CK(hipMemcpyAsync(po.data(), pat->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        if (txt->offsets) CK(hipMemcpyAsync(to.data(), txt->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        if (!max_p) max_p = max_span(po.data(), n);
+        if (txt->offsets && !max_t) max_t = max_span(to.data(), n);
+    }
+    if (!txt->offsets) max_t = txt->length;
+    int rc = nv_tb_checks(al, max_p, max_t, ops_stride);
+    if (rc) return rc;
+    CK(eng->nv_dir.reserve((size_t)max_p * max_t * n + 64));
+    CK(eng->nv_row.reserve((size_t)2 * (max_p + 1) * n * 4 + 64));
+    return gx::nv_traceback_device(*al, n, *pat, *txt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
+                                   scores, sources, sinks, ops, ops_stride, n_ops, st);
+}
+
+int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t n, const gasalx_nv_strings *pat,
+                             uint64_t pat_words, const gasalx_nv_strings *txt, uint64_t txt_words, int32_t *scores,
+                             uint32_t *sources, uint32_t *sinks, uint8_t *ops, uint32_t ops_stride, uint32_t *n_ops) {
+    if (!eng || !al || !pat || !txt || !pat->words || !pat->offsets || !txt->words || !scores || !sources || !sinks ||
+        !ops || !n_ops) {
+        gx::set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    const uint32_t max_p = max_span(pat->offsets, n);
+    const uint32_t max_t = txt->offsets ? max_span(txt->offsets, n) : txt->length;
+    int rc = nv_tb_checks(al, max_p, max_t, ops_stride);
+    if (rc) return rc;
+    gasalx_nv_strings dp = *pat, dt = *txt;
+    uint32_t *p32;
+    if ((rc = stage_in(eng->nv_pw, pat->words, pat_words, st, &p32))) return rc; dp.words = p32;
+    if ((rc = stage_in(eng->nv_po, pat->offsets, (size_t)n + 1, st, &p32))) return rc; dp.offsets = p32;
+    if ((rc = stage_in(eng->nv_tw, txt->words, txt_words, st, &p32))) return rc; dt.words = p32;
+    if ((rc = stage_in(eng->nv_to, txt->offsets, txt->offsets ? (size_t)n + 1 : 0, st, &p32))) return rc;
+    dt.offsets = txt->offsets ? p32 : nullptr;
+    CK(eng->nv_s.reserve((size_t)n * 4));
+    CK(eng->nv_src.reserve((size_t)n * 8));
+    CK(eng->nv_snk.reserve((size_t)n * 8));
+    CK(eng->nv_ops.reserve((size_t)n * ops_stride + 64));
+    CK(eng->nv_nops.reserve((size_t)n * 4));
+    CK(eng->nv_dir.reserve((size_t)max_p * max_t * n + 64));
+    CK(eng->nv_row.reserve((size_t)2 * (max_p + 1) * n * 4 + 64));
+    rc = gx::nv_traceback_device(*al, n, dp, dt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
+                                 eng->nv_s.as<int32_t>(), eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(),
+                                 eng->nv_ops.as<uint8_t>(), ops_stride, eng->nv_nops.as<uint32_t>(), st);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(sources, eng->nv_src.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(sinks, eng->nv_snk.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(ops, eng->nv_ops.p, (size_t)n * ops_stride, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(n_ops, eng->nv_nops.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
     return GASALX_OK;
 }

@@ -1,0 +1,167 @@
+// nvtrace.hpp — nvbio's BatchedAlignmentTraceback (NvB/nvbio/alignment/batched.h:436,
+// batched_inl.h:612-664) on MI355X: the full-DP traceback of the Gotoh and Smith-Waterman
+// aligners, GLOBAL / LOCAL / SEMI_GLOBAL, one pair per thread.
+//
+// The reference runs one thread per job too: a checkpointed scoring pass that keeps the
+// BestSink, then, checkpoint by checkpoint from the sink backwards, a recomputation of the
+// submatrix's direction vectors and the walk through it (alignment_inl.h:365-465).  The
+// checkpoints only bound the reference's storage; the values and flags of every cell are those of
+// one full pass, so here each thread runs that pass once, storing its flags, then walks:
+//   * recurrences and flags: gotoh/gotoh_inl.h:462-593 (PatternBlockingTag update_row: rows i =
+//     text, columns j = pattern; F from the row above = DELETION, E from the left = INSERTION;
+//     hdir = top > left ? (top > diag ? DEL : SUB) : (left > diag ? INS : SUB); extension bits on a
+//     strictly greater extension; LOCAL: H == 0 -> SINK, :441-442) and sw/sw_inl.h:420-540, 380-400;
+//   * boundaries: gotoh_inl.h:695 and the checkpoint context's init (:247-300), sw_inl.h:660-663,
+//     243-251;
+//   * the sink: BestSink keeps the last maximum in report order (stripes of 8 pattern columns,
+//     then rows, then columns) for LOCAL; SEMI_GLOBAL reports H(i, M-1) per row, GLOBAL H(N-1, M-1)
+//     (utils_inl.h:273-300);
+//   * the walk: gotoh_inl.h:1806-1872 (H / E / F states), sw_inl.h:1653-1709, then the first row /
+//     column of alignment_inl.h:442-459.
+// Flags are one byte per cell, interleaved across the launch's threads ([cell][pair]: a wave's
+// stores at one cell are contiguous); the previous row's H and F likewise.  The CPU restatement is
+// oracle/nvbio_oracle.c orc_nv_traceback_one, pinned by nvbio-test's alignment_test.cu:778-792.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gx {
+
+struct NvTbArgs {
+    const uint32_t *pw, *poff;
+    uint32_t pbits, pbig;
+    const uint32_t *tw, *toff;
+    uint32_t tlen0, tbits, tbig;
+    int32_t match, mismatch, go, ge, del, ins;
+    uint32_t n, max_m, max_n;
+    uint8_t *dir;          // [(i * max_m + j)][n]
+    int32_t *row;          // [2 * (max_m + 1)][n]: H(i-1, c) then F(i-1, c), c = -1 .. M-1
+    int32_t *score;
+    uint32_t *src, *snk;   // [2n] each: (x = text, y = pattern)
+    uint8_t *ops;          // pair k's pushes at ops + k * ops_stride (push order)
+    uint32_t ops_stride;
+    uint32_t *n_ops;
+};
+
+__device__ __forceinline__ uint32_t nvtb_symbol(const uint32_t *w, uint32_t bits, uint32_t big, uint32_t s) {
+    const uint32_t per = 32u / bits, p = s % per;
+    const uint32_t sh = big ? 32u - bits * (p + 1u) : bits * p;
+    return (w[s / per] >> sh) & (bits == 32u ? 0xFFFFFFFFu : ((1u << bits) - 1u));
+}
+
+// TYPE: 0 GLOBAL, 1 LOCAL, 2 SEMI_GLOBAL (nvbio AlignmentType)
+template <bool GOTOH, int TYPE>
+__global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.n) return;
+    constexpr uint8_t SUB = 0, INS = 1, DEL = 2, SNK = 3, INS_EXT = 4, DEL_EXT = 8;
+    constexpr uint32_t BAND = 8;   // gotoh_bandlen_selector / the SW stripes: the LOCAL report order
+    const uint32_t p0 = A.poff[k], M = A.poff[k + 1] - p0;
+    const uint32_t t0 = A.toff ? A.toff[k] : 0u, N = A.toff ? A.toff[k + 1] - t0 : A.tlen0;
+    const uint32_t n = A.n;
+    uint32_t *src = A.src + 2 * (size_t)k, *snk = A.snk + 2 * (size_t)k;
+    A.n_ops[k] = 0;
+    if (M == 0 || N == 0 || M > A.max_m || N > A.max_n || M + N > A.ops_stride) {
+        src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
+        A.score[k] = INT32_MIN;
+        return;
+    }
+    const int32_t Go = A.go, Ge = A.ge;
+    const int32_t infimum = -32768 - (Go < Ge ? Go : Ge);
+    int32_t *Hp = A.row + k, *Fp = A.row + (size_t)(A.max_m + 1) * n + k;   // [c + 1][n]
+    auto dcell = [&](uint32_t i, uint32_t j) -> uint8_t & { return A.dir[((size_t)i * A.max_m + j) * n + k]; };
+    for (uint32_t c = 0; c <= M; c++) {
+        const int32_t cc = (int32_t)c - 1;
+        Hp[(size_t)c * n] = TYPE == 1 || cc < 0 ? 0 : GOTOH ? Go + Ge * cc : A.ins * (cc + 1);
+        Fp[(size_t)c * n] = infimum;
+    }
+    int32_t best = INT32_MIN;
+    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu, bblk = 0;
+    for (uint32_t i = 0; i < N; i++) {
+        const uint32_t r = nvtb_symbol(A.tw, A.tbits, A.tbig, t0 + i);
+        const int32_t hl0 = TYPE == 0 ? (GOTOH ? Go + Ge * (int32_t)i : A.del * (int32_t)(i + 1)) : 0;
+        int32_t diagH = Hp[0];
+        int32_t left = hl0;
+        int32_t E = TYPE == 1 ? 0 : infimum;
+        Hp[0] = hl0;
+        for (uint32_t j = 0; j < M; j++) {
+            const uint32_t q = nvtb_symbol(A.pw, A.pbits, A.pbig, p0 + j);
+            const int32_t S = r == q ? A.match : A.mismatch;
+            const int32_t up = Hp[(size_t)(j + 1) * n];
+            int32_t h;
+            uint8_t d;
+            const int32_t diag = diagH + S;
+            if constexpr (GOTOH) {
+                const int32_t ftop = Fp[(size_t)(j + 1) * n] + Ge, htop = up + Go;
+                const int32_t F = max(ftop, htop);
+                const uint8_t fdir = ftop > htop ? DEL_EXT : SUB;
+                const int32_t eleft = E + Ge, hleft = left + Go;
+                E = max(eleft, hleft);
+                const uint8_t edir = eleft > hleft ? INS_EXT : SUB;
+                Fp[(size_t)(j + 1) * n] = F;
+                h = max(max(E, F), diag);
+                if (TYPE == 1) h = max(h, 0);
+                const uint8_t hdir = F > E ? (F > diag ? DEL : SUB) : (E > diag ? INS : SUB);
+                d = (uint8_t)((TYPE == 1 && h == 0 ? SNK : hdir) | edir | fdir);
+            } else {
+                const int32_t top = up + A.del, lft = left + A.ins;
+                h = max(max(top, lft), diag);
+                if (TYPE == 1) h = max(h, 0);
+                const uint8_t hdir = top > lft ? (top > diag ? DEL : SUB) : (lft > diag ? INS : SUB);
+                d = TYPE == 1 && h == 0 ? SNK : hdir;
+            }
+            dcell(i, j) = d;
+            diagH = up;
+            Hp[(size_t)(j + 1) * n] = h;
+            left = h;
+            if (TYPE == 1) {   // report order: stripe, row, column; the last maximum wins
+                const uint32_t blk = j / BAND;
+                if (h > best || (h == best && (blk > bblk || (blk == bblk && (i + 1 > bx || (i + 1 == bx && j + 1 >= by)))))) {
+                    best = h; bx = i + 1; by = j + 1; bblk = blk;
+                }
+            }
+        }
+        if (TYPE == 2 && best <= Hp[(size_t)M * n]) { best = Hp[(size_t)M * n]; bx = i + 1; by = M; }
+    }
+    if (TYPE == 0) { best = Hp[(size_t)M * n]; bx = N; by = M; }
+    snk[0] = bx; snk[1] = by;
+    uint8_t *out = A.ops + (size_t)k * A.ops_stride;
+    int32_t row = (int32_t)bx, col = (int32_t)by - 1;
+    int state = 0;   // H / E / F
+    uint32_t cnt = 0;
+    while (row > 0 && col >= 0) {
+        const uint8_t op = dcell((uint32_t)(row - 1), (uint32_t)col);
+        if constexpr (GOTOH) {
+            const uint8_t h_op = op & 3u;
+            if (TYPE == 1 && state == 0 && h_op == SNK) break;
+            if (state == 1) {
+                if ((op & INS_EXT) == 0) state = 0;
+                --col; out[cnt++] = INS;
+            } else if (state == 2) {
+                if ((op & DEL_EXT) == 0) state = 0;
+                --row; out[cnt++] = DEL;
+            } else if (h_op == INS) {
+                state = 1;
+            } else if (h_op == DEL) {
+                state = 2;
+            } else {
+                --col; --row; out[cnt++] = SUB;
+            }
+        } else {
+            if (TYPE == 1 && op == SNK) break;
+            if (op != DEL) --col;
+            if (op != INS) --row;
+            out[cnt++] = op;
+        }
+    }
+    uint32_t sx = (uint32_t)row, sy = (uint32_t)(col + 1);
+    if (TYPE != 1 && sx == 0)
+        for (; sy > 0; --sy) out[cnt++] = INS;
+    if (TYPE == 0 && sy == 0)
+        for (; sx > 0; --sx) out[cnt++] = DEL;
+    src[0] = sx; src[1] = sy;
+    A.n_ops[k] = cnt;
+    A.score[k] = best;
+}
+
+}  // namespace gx

@@ -34,6 +34,7 @@ EXPORTS = (
     "gasalx_pairhmm_quals_device", "gasalx_pairhmm_quals_host", "gasalx_hmm_file_read", "gasalx_hmm_file_free",
     "gasalx_nv_score_device", "gasalx_nv_score_host", "gasalx_nv_describe_plan",
     "gasalx_nv_banded_score_device", "gasalx_nv_banded_score_host",
+    "gasalx_nv_traceback_device", "gasalx_nv_traceback_host",
     "gasalx_multi_create", "gasalx_multi_destroy", "gasalx_multi_info", "gasalx_multi_engine",
     "gasalx_shard_bounds", "gasalx_multi_align_host", "gasalx_multi_pairhmm_host",
     "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather", "gasalx_packed_pairs",
@@ -380,6 +381,33 @@ class Engine:
                                                  ctypes.c_uint64(len(patterns.words)), ctypes.byref(texts.cstruct()),
                                                  ctypes.c_uint64(len(texts.words)), _p(sc)), "nv_banded_score_host")
         return sc
+
+    def nv_traceback_host(self, aligner: "NvAligner", patterns: "PackedSet", texts: "PackedSet"):
+        """nvbio BatchedAlignmentTraceback (gasalx_nv_traceback_host): per pair the BestSink score, the
+        Alignment's source and sink ((x, y) = (text, pattern)) and the backtracker's pushes in push
+        order (0 'M', 1 'I', 2 'D') -- the dict oracle.nv_traceback returns."""
+        n = patterns.n
+        po = np.asarray(patterns.offsets, np.int64)
+        plen = po[1:] - po[:-1]
+        if texts.offsets is not None:
+            to = np.asarray(texts.offsets, np.int64)
+            tlen = to[1:] - to[:-1]
+        else:
+            tlen = np.full(n, int(texts.length), np.int64)
+        stride = int(plen.max(initial=0) + tlen.max(initial=0))
+        sc = np.zeros(n, np.int32)
+        src = np.zeros(2 * n, np.uint32)
+        snk = np.zeros(2 * n, np.uint32)
+        ops = np.zeros(max(n * stride, 1), np.uint8)
+        nops = np.zeros(n, np.uint32)
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_traceback_host(self._h, ctypes.byref(ca), ctypes.c_uint32(n),
+                                              ctypes.byref(patterns.cstruct()), ctypes.c_uint64(len(patterns.words)),
+                                              ctypes.byref(texts.cstruct()), ctypes.c_uint64(len(texts.words)),
+                                              _p(sc), _p(src), _p(snk), _p(ops), ctypes.c_uint32(stride), _p(nops)),
+               "nv_traceback_host")
+        return dict(score=sc, source=src.reshape(n, 2), sink=snk.reshape(n, 2),
+                    ops=[ops[k * stride:k * stride + int(nops[k])].copy() for k in range(n)])
 
     def nv_banded_score_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
                                     scores_ptr: int, stream: int = 0, max_pattern_len: int = 0):

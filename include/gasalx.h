@@ -283,6 +283,29 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *ali
                                 uint32_t n_pairs, const gasalx_nv_strings *patterns, uint64_t pattern_words,
                                 const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores);
 
+/* nvbio's BatchedAlignmentTraceback<CHECKPOINTS> (NvB/nvbio/alignment/batched.h:436,
+ * batched_inl.h:612-664, alignment_inl.h:365-465): the full-DP traceback of the Gotoh and
+ * Smith-Waterman aligners (GASALX_NV_GOTOH / _SW; edit distance is not offered), GLOBAL / LOCAL /
+ * SEMI_GLOBAL, one pair per thread.  Per pair: the BestSink score, the Alignment's source and
+ * sink as (x, y) = (text, pattern) coordinates in sources[2k..] / sinks[2k..] (0xFFFFFFFF when no
+ * cell was reported), and the backtracker's pushes in push order (end of the alignment first) at
+ * ops + k * ops_stride: 0 SUBSTITUTION ('M'), 1 INSERTION ('I', a pattern symbol), 2 DELETION ('D',
+ * a text symbol); n_ops[k] of them.  nvbio's Backtracer also receives clip(pattern_len - sink.y)
+ * before the pushes and clip(source.y) after them (nvbio_batched.h replays both).
+ * ops_stride >= max pattern + max text length; nvbio's int16 DP columns bound
+ * (max pattern + max text + 2) * max |score| <= 32767, and pattern x text <= 16 M cells.
+ * Workspace: pattern x text bytes + 8 (pattern + 1) bytes per pair, held by the engine. */
+int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
+                               const gasalx_nv_strings *dev_patterns, const gasalx_nv_strings *dev_texts,
+                               uint32_t max_pattern_len, uint32_t max_text_len, int32_t *dev_scores,
+                               uint32_t *dev_sources, uint32_t *dev_sinks, uint8_t *dev_ops, uint32_t ops_stride,
+                               uint32_t *dev_n_ops, void *stream);   /* max lengths: 0 = read back */
+int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
+                             const gasalx_nv_strings *patterns, uint64_t pattern_words,
+                             const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores,
+                             uint32_t *sources, uint32_t *sinks, uint8_t *ops, uint32_t ops_stride,
+                             uint32_t *n_ops);
+
 /* Multi-GPU from one host process.  A group holds one engine per
  * entry of a device list (entries may repeat a device); a host batch is split into
  * contiguous ranges of pairs with equal cell counts (Σ ql·tl; gasalx_shard_bounds),

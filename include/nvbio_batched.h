@@ -15,7 +15,10 @@
  * text in LDS; banded: nvbanded.hpp, one pair per thread with the band in registers);
  * there is no temporary storage, so max_temp_storage() is 0.  The TextBlockingTag /
  * PatternBlockingTag score semantics are provided (both give the same scores), full and
- * banded; nvbio's traceback and warp variants are not.
+ * banded.  Traceback: BatchedAlignmentTraceback<CHECKPOINTS, stream_type> (batched.h:436) for
+ * the Gotoh and Smith-Waterman aligners, full DP, over a TracebackStream (nvtrace.hpp: one
+ * pair per thread, as the reference's DeviceThreadScheduler runs it); the banded traceback and
+ * the warp variants are not provided.
  *
  * Header-only C++ over the flat C-ABI (gasalx.h); link with -lgasal.
  */
@@ -233,6 +236,70 @@ struct BatchedBandedAlignmentScore {
                                                      stream.m_scores32, stream.max_pattern_length(), hip_stream);
         if (rc != GASALX_OK) {
             fprintf(stderr, "BatchedBandedAlignmentScore::enact: %s\n", gasalx_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
+};
+
+// The outputs of a traceback batch (batched_inl.h:612-664's stream.output(): the Alignment
+// and the backtracer of each job), as device arrays: per pair the BestSink score, the
+// Alignment's source and sink as (x = text, y = pattern) pairs, and the backtracker's pushes
+// in push order (end of the alignment first; 0 SUBSTITUTION, 1 INSERTION, 2 DELETION) at
+// ops + k * ops_stride, n_ops[k] of them (ops_stride >= max pattern + max text length).
+enum { SUBSTITUTION = 0, INSERTION = 1, DELETION = 2 };   // alignment_base.h:139-147
+
+template <typename aligner_type_T>
+struct TracebackStream : AlignmentStream<aligner_type_T> {
+    typedef aligner_type_T aligner_type;
+    TracebackStream(const aligner_type aligner, const uint32 count, const uint32 *offsets, const uint32 *patterns,
+                    const uint32 max_pattern_len, const uint32 total_pattern_len, const uint32 *text,
+                    const uint32 text_len, int32 *scores, uint32 *sources, uint32 *sinks, uint8 *ops,
+                    const uint32 ops_stride, uint32 *n_ops)
+        : AlignmentStream<aligner_type_T>(aligner, count, offsets, patterns, max_pattern_len, total_pattern_len,
+                                          text, text_len, nullptr),
+          m_sources(sources), m_sinks(sinks), m_ops(ops), m_ops_stride(ops_stride), m_n_ops(n_ops) {
+        this->m_scores32 = scores;
+    }
+    uint32 *m_sources, *m_sinks;
+    uint8 *m_ops;
+    uint32 m_ops_stride;
+    uint32 *m_n_ops;
+    uint32 m_max_text_len = 0;   // per-pair texts: the longest (0 = read back)
+};
+
+// Feed one job's result (host copies of the stream's outputs) to an nvbio Backtracer (push(op),
+// clip(len)) in the order alignment_traceback calls it (alignment_inl.h:413-462): the end clip,
+// the pushes, the start clip.
+template <typename backtracer_type>
+void replay(backtracer_type &bt, const uint32 pattern_len, const uint32 source_y, const uint32 sink_y,
+            const uint8 *ops, const uint32 n_ops) {
+    bt.clip(pattern_len - sink_y);
+    for (uint32 i = 0; i < n_ops; ++i) bt.push(ops[i]);
+    bt.clip(source_y);
+}
+
+template <uint32 CHECKPOINTS, typename stream_type, typename scheduler_type = DeviceThreadScheduler>
+struct BatchedAlignmentTraceback {
+    typedef stream_type input_stream_type;
+    typedef typename stream_type::aligner_type aligner_type;
+
+    // the workspace (flags of every cell, one DP row per pair) is the engine's, not the caller's
+    static uint64 min_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+    static uint64 max_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+
+    void enact(stream_type stream, uint64 temp_size = 0u, uint8 *temp = NULL, void *hip_stream = NULL) {
+        (void)temp_size; (void)temp;
+        const gasalx_nv_aligner a = stream.aligner().c_aligner();
+        gasalx_nv_strings p = {stream.m_patterns, stream.m_offsets, 0, stream.m_pattern_bits,
+                               stream.m_pattern_big_endian};
+        gasalx_nv_strings t = {stream.m_text, stream.m_text_offsets, stream.m_text_len, stream.m_text_bits,
+                               stream.m_text_big_endian};
+        const int rc = gasalx_nv_traceback_device(engine(), &a, stream.size(), &p, &t, stream.max_pattern_length(),
+                                                  stream.m_text_offsets ? stream.m_max_text_len : stream.m_text_len,
+                                                  stream.m_scores32, stream.m_sources, stream.m_sinks, stream.m_ops,
+                                                  stream.m_ops_stride, stream.m_n_ops, hip_stream);
+        if (rc != GASALX_OK) {
+            fprintf(stderr, "BatchedAlignmentTraceback::enact: %s\n", gasalx_last_error());
             exit(EXIT_FAILURE);
         }
     }

@@ -246,3 +246,175 @@ int orc_nv_banded_score_batch(int aligner, int type, const int32_t prm[6], uint3
     }
     return 0;
 }
+
+/*
+ * Full-DP traceback, one pair (nvbio alignment_traceback, NvB/nvbio/alignment):
+ *   alignment_inl.h:365-465     checkpoint pass with a BestSink, then the walk back from its
+ *                               sink through the checkpointed submatrices, then (SEMI_GLOBAL /
+ *                               GLOBAL) the first row / column, then the clips
+ *   gotoh/gotoh_inl.h:462-593   PatternBlockingTag update_row: rows i = text symbols, columns
+ *                               j = pattern symbols in stripes of BAND_LEN = 8 (:1491-1495);
+ *                               F from the row above (DELETION), E from the left (INSERTION),
+ *                               max3, LOCAL clamp; hdir = top > left ? (top > diag ? DEL : SUB)
+ *                               : (left > diag ? INS : SUB), edir / fdir = strictly greater
+ *                               extension; LOCAL reports every cell (i + 1, block + j) to the sink
+ *   gotoh/gotoh_inl.h:441-442   the stored flags: LOCAL and H == 0 -> SINK, | edir | fdir
+ *   gotoh/gotoh_inl.h:695, 247-300  boundaries: H(-1, c) = LOCAL ? 0 : Go + Ge*c (0 at c = -1),
+ *                               F(-1, c) = infimum; H(i, -1) = GLOBAL ? Go + Ge*i : 0,
+ *                               E(i, -1) = LOCAL ? 0 : infimum (GotohCheckpointContext::init)
+ *   gotoh/gotoh_inl.h:1806-1872 the walk: H state follows hdir (INS -> E state, DEL -> F state,
+ *                               else a diagonal step), E / F states step and leave on a clear
+ *                               extension bit; LOCAL stops on SINK in the H state
+ *   sw/sw_inl.h:420-540, 380-400, 660-663, 243-251, 1653-1709  the same for linear gaps:
+ *                               top = H(i-1, j) + deletion, left = H(i, j-1) + insertion,
+ *                               H(-1, c) = LOCAL ? 0 : insertion*(c+1), H(i, -1) = GLOBAL ?
+ *                               deletion*(i+1) : 0; the walk steps on the stored op
+ *   utils_inl.h:273-300         SEMI_GLOBAL reports H(i, M-1) at (i + 1, M) per row of the last
+ *                               stripe, GLOBAL H(N-1, M-1) at (N, M) once
+ *   sink_inl.h                  BestSink keeps the last maximum (<=) in report order: for LOCAL
+ *                               stripe, then row, then column
+ * ops[] are the backtracker's pushes in push order (end of the alignment first): 0 SUBSTITUTION,
+ * 1 INSERTION (a pattern symbol), 2 DELETION (a text symbol) -- nvbio-test's TestBacktracker
+ * prints "MID"[op] (alignment_test_utils.h:628-645).  src / snk: the Alignment's source and
+ * sink (x = text coordinate, y = pattern coordinate); (0xFFFFFFFF, 0xFFFFFFFF) and no ops when
+ * no cell was reported.  Scores are int32 here; nvbio stores columns and checkpoints as int16
+ * (utils.h:49-64), the same values while they stay within ±32767.
+ */
+int32_t orc_nv_traceback_one(int aligner, int type, const int32_t prm[6], const uint32_t *pat, uint32_t M,
+                             const uint32_t *txt, uint32_t N, uint32_t src[2], uint32_t snk[2], uint8_t *ops,
+                             uint32_t *n_ops) {
+    const int32_t match = prm[0], mismatch = prm[1], Go = prm[2], Ge = prm[3], Del = prm[4], Ins = prm[5];
+    const int gotoh = aligner == ORC_NV_GOTOH;
+    const int32_t infimum = -32768 - (Go < Ge ? Go : Ge);
+    enum { SUB = 0, INS = 1, DEL = 2, SNK = 3, INS_EXT = 4, DEL_EXT = 8 };
+    *n_ops = 0;
+    src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
+    if (M == 0 || N == 0) return INT32_MIN;
+    uint8_t *dir = (uint8_t *)malloc((size_t)M * N);
+    int32_t *Hp = (int32_t *)malloc((M + 1) * sizeof(int32_t));   /* H(i-1, c), c = -1 .. M-1 at [c + 1] */
+    int32_t *Fp = (int32_t *)malloc((M + 1) * sizeof(int32_t));   /* F(i-1, c) at [c + 1] */
+    for (uint32_t c = 0; c <= M; c++) {
+        const int32_t cc = (int32_t)c - 1;
+        Hp[c] = type == ORC_NV_LOCAL || cc < 0 ? 0 : gotoh ? Go + Ge * cc : Ins * (cc + 1);
+        Fp[c] = infimum;
+    }
+    int32_t best = INT32_MIN;
+    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu, bblk = 0;
+    for (uint32_t i = 0; i < N; i++) {
+        const uint32_t r = txt[i];
+        const int32_t hl0 = type == ORC_NV_GLOBAL ? (gotoh ? Go + Ge * (int32_t)i : Del * (int32_t)(i + 1)) : 0;
+        int32_t diagH = Hp[0];                /* H(i-1, -1) */
+        int32_t left = hl0;                   /* H(i, j-1) */
+        int32_t E = type == ORC_NV_LOCAL ? 0 : infimum;
+        Hp[0] = hl0;
+        for (uint32_t j = 0; j < M; j++) {
+            const int32_t S = r == pat[j] ? match : mismatch;
+            const int32_t up = Hp[j + 1];
+            int32_t h, top, lft;
+            uint8_t d;
+            if (gotoh) {
+                const int32_t ftop = Fp[j + 1] + Ge, htop = up + Go;
+                const int32_t F = nmax(ftop, htop);
+                const uint8_t fdir = ftop > htop ? DEL_EXT : SUB;
+                const int32_t eleft = E + Ge, hleft = left + Go;
+                E = nmax(eleft, hleft);
+                const uint8_t edir = eleft > hleft ? INS_EXT : SUB;
+                Fp[j + 1] = F;
+                top = F; lft = E;
+                const int32_t diag = diagH + S;
+                h = nmax(nmax(lft, top), diag);
+                if (type == ORC_NV_LOCAL) h = nmax(h, 0);
+                const uint8_t hdir = top > lft ? (top > diag ? DEL : SUB) : (lft > diag ? INS : SUB);
+                d = (uint8_t)((type == ORC_NV_LOCAL && h == 0 ? SNK : hdir) | edir | fdir);
+            } else {
+                top = up + Del; lft = left + Ins;
+                const int32_t diag = diagH + S;
+                h = nmax(nmax(top, lft), diag);
+                if (type == ORC_NV_LOCAL) h = nmax(h, 0);
+                const uint8_t hdir = top > lft ? (top > diag ? DEL : SUB) : (lft > diag ? INS : SUB);
+                d = (uint8_t)(type == ORC_NV_LOCAL && h == 0 ? SNK : hdir);
+            }
+            dir[(size_t)i * M + j] = d;
+            diagH = up;
+            Hp[j + 1] = h;
+            left = h;
+            if (type == ORC_NV_LOCAL) {   /* report order: stripe, row, column; the last maximum wins */
+                const uint32_t blk = j / NV_BAND;
+                if (h > best || (h == best && (blk > bblk || (blk == bblk && (i + 1 > bx || (i + 1 == bx && j + 1 >= by)))))) {
+                    best = h; bx = i + 1; by = j + 1; bblk = blk;
+                }
+            }
+        }
+        if (type == ORC_NV_SEMI_GLOBAL && best <= Hp[M]) { best = Hp[M]; bx = i + 1; by = M; }
+    }
+    if (type == ORC_NV_GLOBAL) { best = Hp[M]; bx = N; by = M; }
+    snk[0] = bx; snk[1] = by;
+    /* the walk (alignment_inl.h:413-462): row = x, col = y - 1 */
+    int32_t row = (int32_t)bx, col = (int32_t)by - 1;
+    int state = 0;   /* HSTATE / ESTATE / FSTATE */
+    uint32_t k = 0;
+    while (row > 0 && col >= 0) {
+        const uint8_t op = dir[(size_t)(row - 1) * M + (uint32_t)col];
+        if (gotoh) {
+            const uint8_t h_op = op & 3u;
+            if (type == ORC_NV_LOCAL && state == 0 && h_op == SNK) break;
+            if (state == 1) {
+                if ((op & INS_EXT) == 0) state = 0;
+                --col; ops[k++] = INS;
+            } else if (state == 2) {
+                if ((op & DEL_EXT) == 0) state = 0;
+                --row; ops[k++] = DEL;
+            } else if (h_op == INS) {
+                state = 1;
+            } else if (h_op == DEL) {
+                state = 2;
+            } else {
+                --col; --row; ops[k++] = SUB;
+            }
+        } else {
+            if (type == ORC_NV_LOCAL && op == SNK) break;
+            if (op != DEL) --col;
+            if (op != INS) --row;
+            ops[k++] = op;
+        }
+    }
+    uint32_t sx = (uint32_t)row, sy = (uint32_t)(col + 1);
+    if (type != ORC_NV_LOCAL && sx == 0)
+        for (; sy > 0; --sy) ops[k++] = INS;
+    if (type == ORC_NV_GLOBAL && sy == 0)
+        for (; sx > 0; --sx) ops[k++] = DEL;
+    src[0] = sx; src[1] = sy;
+    *n_ops = k;
+    free(dir); free(Hp); free(Fp);
+    return best;
+}
+
+/* n pairs; ops of pair k at ops + k * ops_stride (ops_stride >= M_k + N_k) */
+int orc_nv_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t n,
+                           const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                           const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
+                           int32_t *scores, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
+                           uint32_t *n_ops, int n_threads) {
+    if (!prm || !pw || !poff || !tw || !scores || !src || !snk || !ops || !n_ops) return -1;
+    if (aligner != ORC_NV_GOTOH && aligner != ORC_NV_SW) return -2;
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads)
+#endif
+    for (long k = 0; k < (long)n; k++) {
+        const uint32_t M = poff[k + 1] - poff[k];
+        const uint64_t t0 = toff ? toff[k] : 0;
+        const uint32_t N = toff ? toff[k + 1] - toff[k] : tlen0;
+        uint32_t *p = (uint32_t *)malloc((M + 1) * sizeof(uint32_t));
+        uint32_t *t = (uint32_t *)malloc((N + 1) * sizeof(uint32_t));
+        for (uint32_t i = 0; i < M; i++) p[i] = nv_sym(pw, pbits, pbig, (uint64_t)poff[k] + i);
+        for (uint32_t i = 0; i < N; i++) t[i] = nv_sym(tw, tbits, tbig, t0 + i);
+        scores[k] = M + N <= ops_stride
+                        ? orc_nv_traceback_one(aligner, type, prm, p, M, t, N, src + 2 * k, snk + 2 * k,
+                                               ops + (size_t)k * ops_stride, n_ops + k)
+                        : INT32_MIN;
+        free(p);
+        free(t);
+    }
+    return 0;
+}

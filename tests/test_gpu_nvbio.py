@@ -348,3 +348,56 @@ def test_banded_rejects_bad_band(engine):
         engine.nv_banded_score_host(ALIGNERS[0], 33, P, P)
     with pytest.raises(RuntimeError, match="band length"):
         engine.nv_banded_score_host(ALIGNERS[0], 1, P, P)
+
+
+# ---- BatchedAlignmentTraceback (gasalx_nv_traceback_*, nvtrace.hpp) ----
+def _check_traceback(engine, al, P, T):
+    g = engine.nv_traceback_host(al, P, T)
+    o = O.nv_traceback(al, P, T)
+    assert np.array_equal(g["score"], o["score"]), al
+    assert np.array_equal(g["source"], o["source"]) and np.array_equal(g["sink"], o["sink"]), al
+    bad = [k for k in range(len(g["ops"])) if not np.array_equal(g["ops"][k], o["ops"][k])]
+    assert not bad, f"{len(bad)} pairs' pushes differ, first #{bad[0]} {al}"
+    return g
+
+
+def test_traceback_reference_cigars(engine):
+    # alignment_test.cu:778-792 through the HIP kernel: the reference's CIGAR strings
+    import test_nvbio_oracle as T
+    for c in T._ref_kats()["alignment"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        for shared in (True, False):
+            Tx = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False, shared=shared)
+            g = _check_traceback(engine, T.ref_aligner(c), P, Tx)
+            assert int(g["score"][0]) == c["score"]
+            assert O.nv_cigar_string(g["ops"][0], len(c["pattern"]), g["source"][0][1], g["sink"][0][1]) == c["cigar"]
+
+
+@pytest.mark.parametrize("aligner", [G.NV_SW, G.NV_GOTOH], ids=["sw", "gotoh"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_traceback_random_pairs(engine, aligner, type_):
+    # reads against windows around them (edits, flanks), per-pair texts and one shared text,
+    # 4-bit big-endian patterns and 2-bit texts as sw-benchmark packs them; lengths 1..150
+    rng = np.random.default_rng(500 + 3 * aligner + type_)
+    al = (G.NvAligner(G.NV_GOTOH, type_, 2, -1, -2, -1) if aligner == G.NV_GOTOH
+          else G.NvAligner(G.NV_SW, type_, match=2, mismatch=-1, deletion=-1, insertion=-1))
+    pats, texts = [], []
+    for _ in range(2000):
+        m = int(rng.integers(1, 151))
+        p = rng.integers(0, 4, m)
+        t = np.concatenate([rng.integers(0, 4, int(rng.integers(0, 20))), p, rng.integers(0, 4, int(rng.integers(0, 20)))])
+        t[rng.random(len(t)) < 0.05] = rng.integers(0, 4)
+        pats.append(p); texts.append(t)
+    P = G.PackedSet.pack(pats)
+    _check_traceback(engine, al, P, G.PackedSet.pack(texts, bits=2, big_endian=False))
+    _check_traceback(engine, al, P, G.PackedSet.pack([texts[0]], bits=2, big_endian=False, shared=True))
+
+
+def test_traceback_rejects(engine):
+    # edit distance has no traceback here; scores beyond nvbio's int16 columns are refused
+    P = G.PackedSet.pack([np.zeros(10, np.uint32)])
+    T = G.PackedSet.pack([np.zeros(10, np.uint32)], bits=2, big_endian=False)
+    with pytest.raises(Exception):
+        engine.nv_traceback_host(G.NvAligner(G.NV_ED, G.NV_GLOBAL), P, T)
+    with pytest.raises(Exception):
+        engine.nv_traceback_host(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2000, -1, -2, -1), P, T)

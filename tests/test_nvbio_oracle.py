@@ -256,3 +256,59 @@ def test_banded_matches_textbook(aligner, s, type_):
 def test_banded_short_text_is_skipped():
     al = G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2, -1, -2, -1)
     assert banded_score(al, 5, [0, 1, 2, 3], [0, 1, 2]) == INT32_MIN
+
+
+# ---- BatchedAlignmentTraceback (orc_nv_traceback_*, the checker of nvtrace.hpp) ----
+def _replay_score(al, p, t, ops, src, snk):
+    """The score of the alignment the pushes describe, walked from the source forwards (the
+    TestBacktracker::score idea, alignment_test_utils.h:650-720): Gotoh gaps open once per run."""
+    s, j, k, prev = 0, int(src[1]), int(src[0]), None
+    for op in ops[::-1]:
+        if op == 0:
+            s += al.match if p[j] == t[k] else al.mismatch
+            j += 1; k += 1
+        elif op == 1:
+            s += (al.gap_ext if prev == 1 else al.gap_open) if al.aligner == G.NV_GOTOH else al.insertion
+            j += 1
+        else:
+            s += (al.gap_ext if prev == 2 else al.gap_open) if al.aligner == G.NV_GOTOH else al.deletion
+            k += 1
+        prev = op
+    assert (k, j) == (int(snk[0]), int(snk[1]))
+    return s
+
+
+def test_traceback_reference_cigars():
+    # alignment_test.cu:778-792: SW and Gotoh x GLOBAL / LOCAL / SEMI_GLOBAL traceback strings
+    for c in _ref_kats()["alignment"]:
+        al = ref_aligner(c)
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        r = O.nv_traceback(al, P, T)
+        assert int(r["score"][0]) == c["score"], c
+        got = O.nv_cigar_string(r["ops"][0], len(c["pattern"]), r["source"][0][1], r["sink"][0][1])
+        assert got == c["cigar"], (c, got)
+
+
+@pytest.mark.parametrize("aligner", [G.NV_SW, G.NV_GOTOH], ids=["sw", "gotoh"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_traceback_is_an_optimal_path(aligner, type_):
+    # random pairs: the traceback's score is the score-only pass's (a different blocking of the
+    # same DP), and its pushes, replayed from the source, reach the sink with that score
+    rng = np.random.default_rng(11 + 3 * aligner + type_)
+    s = (2, -3, -5, -2) if aligner == G.NV_GOTOH else (2, -1, 0, 0)
+    al = (G.NvAligner(G.NV_GOTOH, type_, *s) if aligner == G.NV_GOTOH
+          else G.NvAligner(G.NV_SW, type_, match=2, mismatch=-1, deletion=-2, insertion=-2))
+    pats, texts = [], []
+    for _ in range(300):
+        m = int(rng.integers(1, 60))
+        p = rng.integers(0, 4, m)
+        t = np.concatenate([rng.integers(0, 4, int(rng.integers(0, 12))), p, rng.integers(0, 4, int(rng.integers(0, 12)))])
+        t[rng.random(len(t)) < 0.1] = rng.integers(0, 4)
+        pats.append(p); texts.append(t)
+    P = G.PackedSet.pack(pats, bits=2, big_endian=False)
+    T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+    r = O.nv_traceback(al, P, T)
+    assert list(r["score"]) == list(O.nv_score(al, P, T))
+    for k in range(len(pats)):
+        assert _replay_score(al, pats[k], texts[k], r["ops"][k], r["source"][k], r["sink"][k]) == r["score"][k], k
