@@ -316,7 +316,7 @@ int nv_banded_score_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t 
 
 
 // nvbio BatchedAlignmentTraceback (nvtrace.hpp): one pair per thread, flags and the previous row in
-// the caller's workspace (dir: max_p * max_t bytes per pair, row: 2 * (max_p + 1) int32 per pair)
+// the caller's workspace (dir: pad8(max_p) * max_t bytes per pair, row: max_t int2 per pair)
 int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv_strings &pat,
                         const gasalx_nv_strings &txt, uint32_t max_p, uint32_t max_t, uint8_t *dir, int32_t *row,
                         int32_t *score, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,

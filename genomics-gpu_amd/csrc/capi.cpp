@@ -677,8 +677,8 @@ int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *al, 
     if (!txt->offsets) max_t = txt->length;
     int rc = nv_tb_checks(al, max_p, max_t, ops_stride);
     if (rc) return rc;
-    CK(eng->nv_dir.reserve((size_t)max_p * max_t * n + 64));
-    CK(eng->nv_row.reserve((size_t)2 * (max_p + 1) * n * 4 + 64));
+    CK(eng->nv_dir.reserve((size_t)((max_p + 7) / 8) * 8 * max_t * n + 64));
+    CK(eng->nv_row.reserve((size_t)max_t * n * 8 + 64));
     return gx::nv_traceback_device(*al, n, *pat, *txt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
                                    scores, sources, sinks, ops, ops_stride, n_ops, st);
 }
@@ -710,8 +710,8 @@ int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, ui
     CK(eng->nv_snk.reserve((size_t)n * 8));
     CK(eng->nv_ops.reserve((size_t)n * ops_stride + 64));
     CK(eng->nv_nops.reserve((size_t)n * 4));
-    CK(eng->nv_dir.reserve((size_t)max_p * max_t * n + 64));
-    CK(eng->nv_row.reserve((size_t)2 * (max_p + 1) * n * 4 + 64));
+    CK(eng->nv_dir.reserve((size_t)((max_p + 7) / 8) * 8 * max_t * n + 64));
+    CK(eng->nv_row.reserve((size_t)max_t * n * 8 + 64));
     rc = gx::nv_traceback_device(*al, n, dp, dt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
                                  eng->nv_s.as<int32_t>(), eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(),
                                  eng->nv_ops.as<uint8_t>(), ops_stride, eng->nv_nops.as<uint32_t>(), st);

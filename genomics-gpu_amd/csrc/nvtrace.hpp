@@ -18,8 +18,8 @@
 //     (utils_inl.h:273-300);
 //   * the walk: gotoh_inl.h:1806-1872 (H / E / F states), sw_inl.h:1653-1709, then the first row /
 //     column of alignment_inl.h:442-459.
-// Flags are one byte per cell, interleaved across the launch's threads ([cell][pair]: a wave's
-// stores at one cell are contiguous); the previous row's H and F likewise.  The CPU restatement is
+// Flags are one byte per cell, 8 cells of a row and stripe per store, interleaved across the
+// launch's threads ([row][stripe][pair]: a wave's stores are contiguous).  The CPU restatement is
 // oracle/nvbio_oracle.c orc_nv_traceback_one, pinned by nvbio-test's alignment_test.cu:778-792.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -34,8 +34,8 @@ struct NvTbArgs {
     uint32_t tlen0, tbits, tbig;
     int32_t match, mismatch, go, ge, del, ins;
     uint32_t n, max_m, max_n;
-    uint8_t *dir;          // [(i * max_m + j)][n]
-    int32_t *row;          // [2 * (max_m + 1)][n]: H(i-1, c) then F(i-1, c), c = -1 .. M-1
+    uint8_t *dir;          // [text row][stripe of 8 pattern columns][n] x 8 bytes
+    int32_t *row;          // [text row][n] int2: (H, E) of the previous stripe's last column
     int32_t *score;
     uint32_t *src, *snk;   // [2n] each: (x = text, y = pattern)
     uint8_t *ops;          // pair k's pushes at ops + k * ops_stride (push order)
@@ -49,13 +49,18 @@ __device__ __forceinline__ uint32_t nvtb_symbol(const uint32_t *w, uint32_t bits
     return (w[s / per] >> sh) & (bits == 32u ? 0xFFFFFFFFu : ((1u << bits) - 1u));
 }
 
-// TYPE: 0 GLOBAL, 1 LOCAL, 2 SEMI_GLOBAL (nvbio AlignmentType)
+// TYPE: 0 GLOBAL, 1 LOCAL, 2 SEMI_GLOBAL (nvbio AlignmentType).  The pass runs in stripes of 8
+// pattern columns, as the reference's PatternBlockingTag does: a stripe's H and F across its 8
+// columns stay in registers, the (H, E) of its last column goes to the next stripe through one
+// int2 per text row ([row][pair], A.row), and the 8 cells' flags of a row are one 8-byte store
+// ([row][stripe][pair] uint2, A.dir) -- 3 bytes of memory traffic per cell instead of the 17 of
+// a row-by-row pass that kept whole DP rows in memory.
 template <bool GOTOH, int TYPE>
 __global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= A.n) return;
     constexpr uint8_t SUB = 0, INS = 1, DEL = 2, SNK = 3, INS_EXT = 4, DEL_EXT = 8;
-    constexpr uint32_t BAND = 8;   // gotoh_bandlen_selector / the SW stripes: the LOCAL report order
+    constexpr uint32_t BAND = 8;   // gotoh_bandlen_selector / the SW stripes (and the LOCAL report order)
     const uint32_t p0 = A.poff[k], M = A.poff[k + 1] - p0;
     const uint32_t t0 = A.toff ? A.toff[k] : 0u, N = A.toff ? A.toff[k + 1] - t0 : A.tlen0;
     const uint32_t n = A.n;
@@ -68,63 +73,81 @@ __global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
     }
     const int32_t Go = A.go, Ge = A.ge;
     const int32_t infimum = -32768 - (Go < Ge ? Go : Ge);
-    int32_t *Hp = A.row + k, *Fp = A.row + (size_t)(A.max_m + 1) * n + k;   // [c + 1][n]
-    auto dcell = [&](uint32_t i, uint32_t j) -> uint8_t & { return A.dir[((size_t)i * A.max_m + j) * n + k]; };
-    for (uint32_t c = 0; c <= M; c++) {
-        const int32_t cc = (int32_t)c - 1;
-        Hp[(size_t)c * n] = TYPE == 1 || cc < 0 ? 0 : GOTOH ? Go + Ge * cc : A.ins * (cc + 1);
-        Fp[(size_t)c * n] = infimum;
-    }
+    const uint32_t stripes = (A.max_m + BAND - 1) / BAND;
+    int2 *temp = reinterpret_cast<int2 *>(A.row) + k;   // [row][pair]
+    uint2 *dir8 = reinterpret_cast<uint2 *>(A.dir);       // [row][stripe][pair]
+    for (uint32_t i = 0; i < N; i++)   // the first column's left neighbours (the checkpoint context's init)
+        temp[(size_t)i * n] = make_int2(TYPE == 0 ? (GOTOH ? Go + Ge * (int32_t)i : A.del * (int32_t)(i + 1)) : 0,
+                                        TYPE == 1 ? 0 : infimum);
     int32_t best = INT32_MIN;
-    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu, bblk = 0;
-    for (uint32_t i = 0; i < N; i++) {
-        const uint32_t r = nvtb_symbol(A.tw, A.tbits, A.tbig, t0 + i);
-        const int32_t hl0 = TYPE == 0 ? (GOTOH ? Go + Ge * (int32_t)i : A.del * (int32_t)(i + 1)) : 0;
-        int32_t diagH = Hp[0];
-        int32_t left = hl0;
-        int32_t E = TYPE == 1 ? 0 : infimum;
-        Hp[0] = hl0;
-        for (uint32_t j = 0; j < M; j++) {
-            const uint32_t q = nvtb_symbol(A.pw, A.pbits, A.pbig, p0 + j);
-            const int32_t S = r == q ? A.match : A.mismatch;
-            const int32_t up = Hp[(size_t)(j + 1) * n];
-            int32_t h;
-            uint8_t d;
-            const int32_t diag = diagH + S;
-            if constexpr (GOTOH) {
-                const int32_t ftop = Fp[(size_t)(j + 1) * n] + Ge, htop = up + Go;
-                const int32_t F = max(ftop, htop);
-                const uint8_t fdir = ftop > htop ? DEL_EXT : SUB;
-                const int32_t eleft = E + Ge, hleft = left + Go;
-                E = max(eleft, hleft);
-                const uint8_t edir = eleft > hleft ? INS_EXT : SUB;
-                Fp[(size_t)(j + 1) * n] = F;
-                h = max(max(E, F), diag);
-                if (TYPE == 1) h = max(h, 0);
-                const uint8_t hdir = F > E ? (F > diag ? DEL : SUB) : (E > diag ? INS : SUB);
-                d = (uint8_t)((TYPE == 1 && h == 0 ? SNK : hdir) | edir | fdir);
-            } else {
-                const int32_t top = up + A.del, lft = left + A.ins;
-                h = max(max(top, lft), diag);
-                if (TYPE == 1) h = max(h, 0);
-                const uint8_t hdir = top > lft ? (top > diag ? DEL : SUB) : (lft > diag ? INS : SUB);
-                d = TYPE == 1 && h == 0 ? SNK : hdir;
-            }
-            dcell(i, j) = d;
-            diagH = up;
-            Hp[(size_t)(j + 1) * n] = h;
-            left = h;
-            if (TYPE == 1) {   // report order: stripe, row, column; the last maximum wins
-                const uint32_t blk = j / BAND;
-                if (h > best || (h == best && (blk > bblk || (blk == bblk && (i + 1 > bx || (i + 1 == bx && j + 1 >= by)))))) {
-                    best = h; bx = i + 1; by = j + 1; bblk = blk;
-                }
-            }
+    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu;
+    int32_t last_h = 0;   // H(i, M-1) of the stripe holding column M-1
+    for (uint32_t blk = 0; blk * BAND < M; blk++) {
+        const uint32_t c0 = blk * BAND;
+        uint32_t q[BAND];
+        int32_t Hb[BAND + 1], Fb[BAND + 1];
+#pragma unroll
+        for (uint32_t j = 0; j < BAND; j++) q[j] = c0 + j < M ? nvtb_symbol(A.pw, A.pbits, A.pbig, p0 + c0 + j) : 0xFFFFu;
+#pragma unroll
+        for (uint32_t j = 0; j <= BAND; j++) {   // row -1: H(-1, c0 + j - 1)
+            const int32_t cc = (int32_t)(c0 + j) - 1;
+            Hb[j] = TYPE == 1 || cc < 0 ? 0 : GOTOH ? Go + Ge * cc : A.ins * (cc + 1);
+            Fb[j] = infimum;
         }
-        if (TYPE == 2 && best <= Hp[(size_t)M * n]) { best = Hp[(size_t)M * n]; bx = i + 1; by = M; }
+        int32_t diag0 = Hb[0];
+        for (uint32_t i = 0; i < N; i++) {
+            const uint32_t r = nvtb_symbol(A.tw, A.tbits, A.tbig, t0 + i);
+            const int2 tv = temp[(size_t)i * n];
+            int32_t diagH = diag0;     // H(i-1, c0-1)
+            diag0 = tv.x;
+            Hb[0] = tv.x;              // H(i, c0-1)
+            int32_t E = tv.y;          // E(i, c0-1)
+            uint32_t flo = 0, fhi = 0;
+#pragma unroll
+            for (uint32_t j = 1; j <= BAND; j++) {
+                const int32_t S = r == q[j - 1] ? A.match : A.mismatch;
+                const int32_t up = Hb[j];
+                const int32_t diag = diagH + S;
+                int32_t h;
+                uint32_t d;
+                if constexpr (GOTOH) {
+                    const int32_t ftop = Fb[j] + Ge, htop = up + Go;
+                    const int32_t F = max(ftop, htop);
+                    const uint32_t fdir = ftop > htop ? DEL_EXT : SUB;
+                    const int32_t eleft = E + Ge, hleft = Hb[j - 1] + Go;
+                    E = max(eleft, hleft);
+                    const uint32_t edir = eleft > hleft ? INS_EXT : SUB;
+                    Fb[j] = F;
+                    h = max(max(E, F), diag);
+                    if (TYPE == 1) h = max(h, 0);
+                    const uint32_t hdir = F > E ? (F > diag ? DEL : SUB) : (E > diag ? INS : SUB);
+                    d = (TYPE == 1 && h == 0 ? SNK : hdir) | edir | fdir;
+                } else {
+                    const int32_t top = up + A.del, lft = Hb[j - 1] + A.ins;
+                    h = max(max(top, lft), diag);
+                    if (TYPE == 1) h = max(h, 0);
+                    const uint32_t hdir = top > lft ? (top > diag ? DEL : SUB) : (lft > diag ? INS : SUB);
+                    d = TYPE == 1 && h == 0 ? SNK : hdir;
+                }
+                diagH = up;
+                Hb[j] = h;
+                if (j <= 4) flo |= d << (8 * (j - 1)); else fhi |= d << (8 * (j - 5));
+                if (TYPE == 1 && c0 + j <= M && best <= h) {   // report order: stripe, row, column; the last maximum wins
+                    best = h; bx = i + 1; by = c0 + j;
+                }
+                if (c0 + j == M) last_h = h;
+            }
+            dir8[((size_t)i * stripes + blk) * n + k] = make_uint2(flo, fhi);
+            temp[(size_t)i * n] = make_int2(Hb[BAND], E);
+            if (TYPE == 2 && c0 + BAND >= M && best <= last_h) { best = last_h; bx = i + 1; by = M; }
+        }
     }
-    if (TYPE == 0) { best = Hp[(size_t)M * n]; bx = N; by = M; }
+    if (TYPE == 0) { best = last_h; bx = N; by = M; }
     snk[0] = bx; snk[1] = by;
+    const uint8_t *dir = A.dir;
+    auto dcell = [&](uint32_t i, uint32_t j) -> uint8_t {
+        return dir[(((size_t)i * stripes + j / BAND) * n + k) * 8 + (j % BAND)];
+    };
     uint8_t *out = A.ops + (size_t)k * A.ops_stride;
     int32_t row = (int32_t)bx, col = (int32_t)by - 1;
     int state = 0;   // H / E / F

@@ -409,6 +409,20 @@ class Engine:
         return dict(score=sc, source=src.reshape(n, 2), sink=snk.reshape(n, 2),
                     ops=[ops[k * stride:k * stride + int(nops[k])].copy() for k in range(n)])
 
+    def nv_traceback_device_ptrs(self, aligner: "NvAligner", n: int, pat: dict, txt: dict, outs: dict,
+                                 ops_stride: int, max_pattern_len: int = 0, max_text_len: int = 0, stream: int = 0):
+        """Device-resident traceback (gasalx_nv_traceback_device); pat/txt as nv_score_device_ptrs, outs =
+        {"score", "source", "sink", "ops", "n_ops"} device addresses."""
+        mk = lambda d: CNvStrings(d["words"], d.get("offsets") or None, d.get("length", 0), d["bits"],
+                                  int(d.get("big_endian", False)))
+        ca = aligner.cstruct()
+        v = lambda k: ctypes.c_void_p(outs[k] or None)
+        _check(lib().gasalx_nv_traceback_device(self._h, ctypes.byref(ca), ctypes.c_uint32(n), ctypes.byref(mk(pat)),
+                                                ctypes.byref(mk(txt)), ctypes.c_uint32(max_pattern_len),
+                                                ctypes.c_uint32(max_text_len), v("score"), v("source"), v("sink"),
+                                                v("ops"), ctypes.c_uint32(ops_stride), v("n_ops"),
+                                                ctypes.c_void_p(stream or None)), "nv_traceback_device")
+
     def nv_banded_score_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
                                     scores_ptr: int, stream: int = 0, max_pattern_len: int = 0):
         """Device-resident banded scoring (gasalx_nv_banded_score_device); pat/txt as nv_score_device_ptrs."""

@@ -294,7 +294,7 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *ali
  * before the pushes and clip(source.y) after them (nvbio_batched.h replays both).
  * ops_stride >= max pattern + max text length; nvbio's int16 DP columns bound
  * (max pattern + max text + 2) * max |score| <= 32767, and pattern x text <= 16 M cells.
- * Workspace: pattern x text bytes + 8 (pattern + 1) bytes per pair, held by the engine. */
+ * Workspace: pad8(pattern) x text bytes + 8 bytes per text symbol per pair, held by the engine. */
 int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
                                const gasalx_nv_strings *dev_patterns, const gasalx_nv_strings *dev_texts,
                                uint32_t max_pattern_len, uint32_t max_text_len, int32_t *dev_scores,

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Throughput of the nvbio BatchedAlignmentTraceback front-end (gasalx_nv_traceback_device,
+nvtrace.hpp) on MI355X: reads of 150 bp drawn from per-pair text windows of 150 + slack symbols
+(4-bit big-endian patterns, 2-bit texts, the sw-benchmark packing), inputs resident in HBM, timed
+with HIP events around the device call; the first pairs' outputs are checked against
+oracle/nvbio_oracle.c (test infrastructure).  Prints one JSON line per aligner/type.
+
+usage: nv_traceback_probe.py [pairs] [slack]"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "genomics-gpu_amd"))
+sys.path.insert(0, ROOT)
+import gasal_ffi as G  # noqa: E402
+import oracle.oracle as O  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    slack = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+    rng = np.random.default_rng(0x5EED0077)
+    m = 150
+    texts = rng.integers(0, 4, (n, m + slack))
+    st = rng.integers(0, slack + 1, n)
+    pats = texts[np.arange(n)[:, None], st[:, None] + np.arange(m)[None, :]].copy()
+    flip = rng.random(pats.shape) < 0.03
+    pats[flip] = (pats[flip] + rng.integers(1, 4, int(flip.sum()))) % 4
+    P = G.PackedSet.pack(list(pats))
+    T = G.PackedSet.pack(list(texts), bits=2, big_endian=False)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    pw, po, tw, to = t(P.words), t(P.offsets), t(T.words), t(T.offsets)
+    stride = m + m + slack
+    outs_t = dict(score=torch.zeros(n, dtype=torch.int32, device=dev), source=torch.zeros(2 * n, dtype=torch.int32, device=dev),
+                  sink=torch.zeros(2 * n, dtype=torch.int32, device=dev), ops=torch.zeros(n * stride, dtype=torch.uint8, device=dev),
+                  n_ops=torch.zeros(n, dtype=torch.int32, device=dev))
+    outs = {k: v.data_ptr() for k, v in outs_t.items()}
+    pat = dict(words=pw.data_ptr(), offsets=po.data_ptr(), bits=4, big_endian=True)
+    txt = dict(words=tw.data_ptr(), offsets=to.data_ptr(), bits=2, big_endian=False)
+    eng = G.Engine(0)
+    ts = torch.cuda.Stream()      # a real stream: the null stream's handle 0 would mean the engine's own
+    s = ts.cuda_stream
+    cells = n * m * (m + slack)
+    for name, al in (("gotoh_local", G.NvAligner(G.NV_GOTOH, G.NV_LOCAL, 2, -1, -2, -1)),
+                     ("gotoh_semi", G.NvAligner(G.NV_GOTOH, G.NV_SEMI_GLOBAL, 2, -1, -2, -1)),
+                     ("gotoh_global", G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2, -1, -2, -1)),
+                     ("sw_local", G.NvAligner(G.NV_SW, G.NV_LOCAL, match=2, mismatch=-1, deletion=-1, insertion=-1))):
+        call = lambda: eng.nv_traceback_device_ptrs(al, n, pat, txt, outs, stride, m, m + slack, s)
+        for _ in range(2):
+            call()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 5
+        e0.record(ts)
+        for _ in range(reps):
+            call()
+        e1.record(ts)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        k = 500
+        o = O.nv_traceback(al, G.PackedSet.pack(list(pats[:k])), G.PackedSet.pack(list(texts[:k]), bits=2, big_endian=False))
+        g_sc = outs_t["score"][:k].cpu().numpy()
+        g_ops = outs_t["ops"][:k * stride].cpu().numpy().reshape(k, stride)
+        g_n = outs_t["n_ops"][:k].cpu().numpy()
+        bad = int((g_sc != o["score"]).sum()) + sum(int(not np.array_equal(g_ops[i, :g_n[i]], o["ops"][i])) for i in range(k))
+        print(json.dumps({"probe": "nv_traceback", "aligner": name, "pairs": n, "pattern": m, "text": m + slack,
+                          "ms": round(ms, 3), "gcups": round(cells / ms / 1e6, 1), "checked": k, "mismatches": bad,
+                          "kernel": "nv_traceback_kernel (one pair per thread, full DP + walk)"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
