@@ -321,9 +321,9 @@ int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv
                         const gasalx_nv_strings &txt, uint32_t max_p, uint32_t max_t, uint8_t *dir, int32_t *row,
                         int32_t *score, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
                         uint32_t *n_ops, hipStream_t st) {
-    if (al.aligner != NV_GOTOH && al.aligner != NV_SW) {
-        set_error("traceback: Gotoh and Smith-Waterman aligners only");
-        return GASALX_EUNSUPPORTED;
+    if (al.aligner != NV_GOTOH && al.aligner != NV_SW && al.aligner != NV_ED) {
+        set_error("traceback: unknown aligner");
+        return GASALX_EINVAL;
     }
     if (al.type < 0 || al.type > 2) { set_error("bad alignment type"); return GASALX_EINVAL; }
     for (uint32_t b : {pat.bits, txt.bits})
@@ -339,6 +339,7 @@ int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv
     A.tbig = txt.big_endian;
     A.match = al.match; A.mismatch = al.mismatch; A.go = al.gap_open; A.ge = al.gap_ext;
     A.del = al.deletion; A.ins = al.insertion;
+    if (al.aligner == NV_ED) { A.match = 0; A.mismatch = -1; A.del = -1; A.ins = -1; }   // ed_inl.h:347-365
     A.n = n; A.max_m = max_p; A.max_n = max_t;
     A.dir = dir; A.row = row; A.score = score; A.src = src; A.snk = snk; A.ops = ops; A.ops_stride = ops_stride;
     A.n_ops = n_ops;
@@ -346,6 +347,47 @@ int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv
     static const Fn tab[2][3] = {{&nv_traceback_kernel<false, 0>, &nv_traceback_kernel<false, 1>, &nv_traceback_kernel<false, 2>},
                                  {&nv_traceback_kernel<true, 0>, &nv_traceback_kernel<true, 1>, &nv_traceback_kernel<true, 2>}};
     hipLaunchKernelGGL(tab[al.aligner == NV_GOTOH ? 1 : 0][al.type], dim3((n + 255) / 256), dim3(256), 0, st, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
+    return GASALX_OK;
+}
+
+// BatchedBandedAlignmentTraceback<band> (nvtrace.hpp nv_banded_traceback_kernel); ED runs as
+// SW with EditDistanceSWScheme (ed_banded_inl.h:175-295).  The band's register arrays come in
+// 8, 16 and 32 cells; the band length itself is a kernel argument.
+int nv_banded_traceback_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
+                               const gasalx_nv_strings &txt, uint32_t max_p, uint32_t *dir, int32_t *score,
+                               uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride, uint32_t *n_ops,
+                               hipStream_t st) {
+    if (al.aligner != NV_GOTOH && al.aligner != NV_SW && al.aligner != NV_ED) {
+        set_error("banded traceback: unknown aligner");
+        return GASALX_EINVAL;
+    }
+    if (al.type < 0 || al.type > 2) { set_error("bad alignment type"); return GASALX_EINVAL; }
+    if (band < 2 || band > 32) { set_error("band length must be 2..32"); return GASALX_EINVAL; }
+    for (uint32_t b : {pat.bits, txt.bits})
+        if (b != 2 && b != 4 && b != 8) { set_error("symbol bits must be 2, 4 or 8"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    if (!pat.words || !pat.offsets || !txt.words || !score || !src || !snk || !ops || !n_ops || !dir) {
+        set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    NvBandTbArgs A;
+    A.pw = pat.words; A.poff = pat.offsets; A.pbits = pat.bits; A.pbig = pat.big_endian;
+    A.tw = txt.words; A.toff = txt.offsets; A.tlen0 = txt.offsets ? 0 : txt.length; A.tbits = txt.bits;
+    A.tbig = txt.big_endian;
+    A.match = al.match; A.mismatch = al.mismatch; A.go = al.gap_open; A.ge = al.gap_ext;
+    A.del = al.deletion; A.ins = al.insertion;
+    if (al.aligner == NV_ED) { A.match = 0; A.mismatch = -1; A.del = -1; A.ins = -1; }
+    A.n = n; A.band = band; A.words = (band + 3) / 4; A.max_m = max_p;
+    A.dir = dir; A.score = score; A.src = src; A.snk = snk; A.ops = ops; A.ops_stride = ops_stride; A.n_ops = n_ops;
+    using Fn = void (*)(NvBandTbArgs);
+#define NVBT_ROW(G, T) {&nv_banded_traceback_kernel<G, T, 8>, &nv_banded_traceback_kernel<G, T, 16>, &nv_banded_traceback_kernel<G, T, 32>}
+    static const Fn tab[2][3][3] = {{NVBT_ROW(false, 0), NVBT_ROW(false, 1), NVBT_ROW(false, 2)},
+                                    {NVBT_ROW(true, 0), NVBT_ROW(true, 1), NVBT_ROW(true, 2)}};
+#undef NVBT_ROW
+    const int cls = band <= 8 ? 0 : band <= 16 ? 1 : 2;
+    hipLaunchKernelGGL(tab[al.aligner == NV_GOTOH ? 1 : 0][al.type][cls], dim3((n + 255) / 256), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
     return GASALX_OK;

@@ -645,10 +645,15 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *al,
 
 // nvbio BatchedAlignmentTraceback (nvtrace.hpp).  nvbio keeps its DP columns and checkpoints in
 // int16 (alignment/utils.h:49-64): the scores of every cell must stay within them.
+static int64_t nv_score_mag(const gasalx_nv_aligner *al) {
+    if (al->aligner == GASALX_NV_ED) return 1;   // ED: EditDistanceSWScheme's 0 / -1 (ed_utils.h:45-52)
+    return std::max<int64_t>({std::abs((int64_t)al->match), std::abs((int64_t)al->mismatch),
+                              std::abs((int64_t)al->gap_open), std::abs((int64_t)al->gap_ext),
+                              std::abs((int64_t)al->deletion), std::abs((int64_t)al->insertion), 1});
+}
+
 static int nv_tb_checks(const gasalx_nv_aligner *al, uint32_t max_p, uint32_t max_t, uint32_t ops_stride) {
-    const int64_t mag = std::max<int64_t>({std::abs((int64_t)al->match), std::abs((int64_t)al->mismatch),
-                                           std::abs((int64_t)al->gap_open), std::abs((int64_t)al->gap_ext),
-                                           std::abs((int64_t)al->deletion), std::abs((int64_t)al->insertion), 1});
+    const int64_t mag = nv_score_mag(al);
     if (((int64_t)max_p + max_t + 2) * mag > 32767) {
         gx::set_error("traceback: scores would leave nvbio's int16 columns (lengths x |score|)");
         return GASALX_ERANGE;
@@ -715,6 +720,83 @@ int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, ui
     rc = gx::nv_traceback_device(*al, n, dp, dt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
                                  eng->nv_s.as<int32_t>(), eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(),
                                  eng->nv_ops.as<uint8_t>(), ops_stride, eng->nv_nops.as<uint32_t>(), st);
+    if (rc) { (void)hipStreamSynchronize(st); return rc; }
+    CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(sources, eng->nv_src.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(sinks, eng->nv_snk.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(ops, eng->nv_ops.p, (size_t)n * ops_stride, hipMemcpyDeviceToHost, st));
+    CK(hipMemcpyAsync(n_ops, eng->nv_nops.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    return GASALX_OK;
+}
+
+// nvbio BatchedBandedAlignmentTraceback<band> (nvtrace.hpp).  nvbio's checkpoints are int16
+// pairs clamped at -32736 (gotoh_banded_inl.h:234-239): every score must stay above it.
+static int nv_btb_checks(const gasalx_nv_aligner *al, uint32_t band, uint32_t max_p, uint32_t ops_stride) {
+    if (band < 2 || band > 32) { gx::set_error("band length must be 2..32"); return GASALX_EINVAL; }
+    if (((int64_t)max_p + band + 3) * nv_score_mag(al) > 32736) {
+        gx::set_error("banded traceback: scores would leave nvbio's int16 checkpoints (lengths x |score|)");
+        return GASALX_ERANGE;
+    }
+    if ((uint64_t)ops_stride < 2ull * max_p + band) {
+        gx::set_error("banded traceback: ops_stride < 2 x max pattern length + band");
+        return GASALX_EINVAL;
+    }
+    return GASALX_OK;
+}
+
+int gasalx_nv_banded_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
+                                      const gasalx_nv_strings *pat, const gasalx_nv_strings *txt, uint32_t max_p,
+                                      int32_t *scores, uint32_t *sources, uint32_t *sinks, uint8_t *ops,
+                                      uint32_t ops_stride, uint32_t *n_ops, void *stream) {
+    if (!eng || !al || !pat || !txt) { gx::set_error("null argument"); return GASALX_EINVAL; }
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = stream ? (hipStream_t)stream : eng->stream;
+    if (!max_p) {   // read the offsets back (synchronises the stream)
+        std::vector<uint32_t> po(n + 1);
+        CK(hipMemcpyAsync(po.data(), pat->offsets, (n + 1) * 4ull, hipMemcpyDeviceToHost, st));
+        CK(hipStreamSynchronize(st));
+        max_p = max_span(po.data(), n);
+    }
+    int rc = nv_btb_checks(al, band, max_p, ops_stride);
+    if (rc) return rc;
+    CK(eng->nv_dir.reserve((size_t)max_p * ((band + 3) / 4) * 4 * n + 64));
+    return gx::nv_banded_traceback_device(*al, band, n, *pat, *txt, max_p, eng->nv_dir.as<uint32_t>(), scores, sources,
+                                          sinks, ops, ops_stride, n_ops, st);
+}
+
+int gasalx_nv_banded_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
+                                    const gasalx_nv_strings *pat, uint64_t pat_words, const gasalx_nv_strings *txt,
+                                    uint64_t txt_words, int32_t *scores, uint32_t *sources, uint32_t *sinks,
+                                    uint8_t *ops, uint32_t ops_stride, uint32_t *n_ops) {
+    if (!eng || !al || !pat || !txt || !pat->words || !pat->offsets || !txt->words || !scores || !sources || !sinks ||
+        !ops || !n_ops) {
+        gx::set_error("null argument");
+        return GASALX_EINVAL;
+    }
+    const uint32_t max_p = n ? max_span(pat->offsets, n) : 0;
+    int rc = nv_btb_checks(al, band, max_p, ops_stride);
+    if (rc) return rc;
+    if (n == 0) return GASALX_OK;
+    CK(hipSetDevice(eng->device));
+    hipStream_t st = eng->stream;
+    gasalx_nv_strings dp = *pat, dt = *txt;
+    uint32_t *p32;
+    if ((rc = stage_in(eng->nv_pw, pat->words, pat_words, st, &p32))) return rc; dp.words = p32;
+    if ((rc = stage_in(eng->nv_po, pat->offsets, (size_t)n + 1, st, &p32))) return rc; dp.offsets = p32;
+    if ((rc = stage_in(eng->nv_tw, txt->words, txt_words, st, &p32))) return rc; dt.words = p32;
+    if ((rc = stage_in(eng->nv_to, txt->offsets, txt->offsets ? (size_t)n + 1 : 0, st, &p32))) return rc;
+    dt.offsets = txt->offsets ? p32 : nullptr;
+    CK(eng->nv_s.reserve((size_t)n * 4));
+    CK(eng->nv_src.reserve((size_t)n * 8));
+    CK(eng->nv_snk.reserve((size_t)n * 8));
+    CK(eng->nv_ops.reserve((size_t)n * ops_stride + 64));
+    CK(eng->nv_nops.reserve((size_t)n * 4));
+    CK(eng->nv_dir.reserve((size_t)max_p * ((band + 3) / 4) * 4 * n + 64));
+    rc = gx::nv_banded_traceback_device(*al, band, n, dp, dt, max_p, eng->nv_dir.as<uint32_t>(), eng->nv_s.as<int32_t>(),
+                                        eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(), eng->nv_ops.as<uint8_t>(),
+                                        ops_stride, eng->nv_nops.as<uint32_t>(), st);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(sources, eng->nv_src.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));

@@ -141,6 +141,10 @@ int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv
                         const gasalx_nv_strings &txt, uint32_t max_p, uint32_t max_t, uint8_t *dir, int32_t *row,
                         int32_t *score, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
                         uint32_t *n_ops, hipStream_t st);
+int nv_banded_traceback_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
+                               const gasalx_nv_strings &txt, uint32_t max_p, uint32_t *dir, int32_t *score,
+                               uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride, uint32_t *n_ops,
+                               hipStream_t st);
 std::string nv_plan_name(const gasalx_nv_aligner &al, uint32_t max_p, uint32_t max_t, bool per_pair_text,
                          uint32_t text_bits);
 

@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "nvbio.hpp"
+#include "nvbio16.hpp"   // pk_max3 (nv_banded16_kernel)
 
 namespace gx {
 

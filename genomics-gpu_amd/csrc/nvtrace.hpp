@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "nvbanded.hpp"   // NvSymReader
+
 namespace gx {
 
 struct NvTbArgs {
@@ -185,6 +187,185 @@ __global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
     src[0] = sx; src[1] = sy;
     A.n_ops[k] = cnt;
     A.score[k] = best;
+}
+
+// nvbio's BatchedBandedAlignmentTraceback<BAND_LEN, CHECKPOINTS> (batched.h:464,
+// batched_banded_inl.h:248-297, banded_inl.h:352-427): one pair per thread, the band of B cells
+// of the current pattern row in registers as in nv_banded_kernel (rows i = pattern symbols,
+// entry j = text symbol i + j).  The reference scores with checkpoints, then recomputes each
+// CHECKPOINTS-row window of flags and walks it; the flags are those of one pass, so the pass
+// runs once and stores them (one byte per cell, 4 cells per word, [row][word][pair]: a wave's
+// stores are contiguous), then the thread walks them:
+//   * cells and flags: gotoh/gotoh_banded_inl.h:482-614, :323-339 (top = F = INSERTION, left =
+//     E = DELETION; j = 0 has no E, j = B-1 no F; the E flag of cell j is cell j-1's update;
+//     LOCAL and H == 0 -> SINK) and sw/sw_banded_inl.h:392-475, :268-279 (top + deletion, left +
+//     insertion; the SW flags never hold SINK);
+//   * the sink: LOCAL every cell in row-then-entry order, SEMI_GLOBAL the last row's entries
+//     j < min(M + B - 1, N) - (M - 1), GLOBAL entry B-1; the last maximum wins;
+//   * the walk: gotoh_banded_inl.h:895-962, sw_banded_inl.h:740-798.
+// The CPU restatement is oracle/nvbio_oracle.c orc_nv_banded_traceback_one, pinned by
+// alignment_test.cu:790-793 and :796-826 (4M1D3M with band 7, 147M2D3M with band 31).
+struct NvBandTbArgs {
+    const uint32_t *pw, *poff;
+    uint32_t pbits, pbig;
+    const uint32_t *tw, *toff;
+    uint32_t tbits, tbig, tlen0;
+    int32_t match, mismatch, go, ge, del, ins;
+    uint32_t n, band, words, max_m;   // words = (band + 3) / 4 flag words per row
+    uint32_t *dir;                     // [pattern row][word][n]
+    int32_t *score;
+    uint32_t *src, *snk;
+    uint8_t *ops;
+    uint32_t ops_stride;
+    uint32_t *n_ops;
+};
+
+template <bool GOTOH, int TYPE, int BMAX>
+__global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.n) return;
+    constexpr uint32_t SUB = 0, INS = 1, DEL = 2, SNK = 3, INS_EXT = 4, DEL_EXT = 8;
+    const uint32_t po = A.poff[k], M = A.poff[k + 1] - po;
+    const bool shared = A.toff == nullptr;
+    const uint32_t to = shared ? 0u : A.toff[k], N = shared ? A.tlen0 : A.toff[k + 1] - to;
+    const uint32_t B = A.band, n = A.n;
+    uint32_t *src = A.src + 2 * (size_t)k, *snk = A.snk + 2 * (size_t)k;
+    src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
+    A.n_ops[k] = 0;
+    if (N < M || M > A.max_m || 2 * M + B > A.ops_stride) { A.score[k] = INT32_MIN; return; }
+    const int32_t S_eq = A.match, S_ne = A.mismatch, Go = A.go, Ge = A.ge, Del = A.del, Ins = A.ins;
+    const int32_t infimum = -32768 - max(Go, Ge);   // gotoh_banded_inl.h:446-448
+    int32_t H[BMAX], F[BMAX];
+    uint32_t tc[BMAX];
+    NvSymReader pr, tr;
+    pr.init(A.pw, A.pbits, A.pbig, po, M);
+    tr.init(A.tw, A.tbits, A.tbig, to, N);
+#pragma unroll
+    for (int j = 0; j < BMAX; ++j) {
+        if (GOTOH) H[j] = j == 0 ? 0 : (TYPE == 0 ? Go + (j - 1) * Ge : 0);
+        else H[j] = TYPE == 0 ? j * Del : 0;
+        F[j] = infimum;
+        tc[j] = 255u;
+    }
+    uint32_t tnext = 0;
+#pragma unroll
+    for (int j = 0; j < BMAX - 1; ++j)
+        if ((uint32_t)j + 1 < B) { tc[j] = tnext < N ? tr.next() : 255u; ++tnext; }
+    int32_t best = INT32_MIN;
+    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < M; ++i) {
+        const uint32_t q = pr.next();
+        const uint32_t g_last = tnext < N ? tr.next() : 255u;
+        ++tnext;
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j)
+            if ((uint32_t)j + 1 == B) tc[j] = g_last;
+        int32_t E = 0, hprev = 0;
+        uint32_t edir = SUB;
+        uint32_t fw[BMAX / 4];
+#pragma unroll
+        for (int w = 0; w < BMAX / 4; ++w) fw[w] = 0;
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j) {
+            if ((uint32_t)j >= B) break;
+            const bool last = (uint32_t)j + 1 == B;
+            const int jn = j + 1 < BMAX ? j + 1 : j;
+            const int32_t diag = H[j] + (tc[j] == q ? S_eq : S_ne);
+            int32_t hi;
+            uint32_t d;
+            if (GOTOH) {
+                uint32_t fdir = SUB;
+                if (!last) {
+                    const int32_t ftop = F[jn] + Ge, htop = H[jn] + Go;
+                    F[j] = max(ftop, htop);
+                    fdir = ftop > htop ? DEL_EXT : SUB;
+                } else {
+                    F[j] = infimum;
+                }
+                uint32_t hdir;
+                if (j == 0) { hi = max(F[0], diag); hdir = F[0] > diag ? INS : SUB; }
+                else if (!last) { hi = max(max(F[j], E), diag); hdir = F[j] > E ? (F[j] > diag ? INS : SUB) : (E > diag ? DEL : SUB); }
+                else { hi = max(E, diag); hdir = E > diag ? DEL : SUB; }
+                if (TYPE == 1) {
+                    hi = max(hi, 0);
+                    if (hi == 0) hdir = SNK;
+                    if (best <= hi) { best = hi; bx = i + j + 1; by = i + 1; }
+                }
+                d = hdir | (j == 0 ? SUB : edir) | fdir;
+                H[j] = hi;
+                if (j == 0) { E = hi + Go; edir = SUB; }
+                else {
+                    const int32_t eleft = E + Ge, ediag = hi + Go;
+                    edir = eleft > ediag ? INS_EXT : SUB;
+                    E = max(ediag, eleft);
+                }
+            } else {
+                const int32_t top = H[jn] + Del, left = hprev + Ins;
+                if (j == 0) { hi = max(top, diag); d = top > diag ? INS : SUB; }
+                else if (!last) { hi = max(max(top, left), diag); d = top > left ? (top > diag ? INS : SUB) : (left > diag ? DEL : SUB); }
+                else { hi = max(left, diag); d = left > diag ? DEL : SUB; }
+                if (TYPE == 1) {
+                    hi = max(hi, 0);
+                    if (best <= hi) { best = hi; bx = i + j + 1; by = i + 1; }
+                }
+                H[j] = hi;
+                hprev = hi;
+            }
+            fw[j / 4] |= d << (8 * (j % 4));
+        }
+#pragma unroll
+        for (int w = 0; w < BMAX / 4; ++w)
+            if ((uint32_t)w < A.words) A.dir[((size_t)i * A.words + w) * n + k] = fw[w];
+#pragma unroll
+        for (int j = 0; j + 1 < BMAX; ++j)
+            if ((uint32_t)j + 1 < B) tc[j] = tc[j + 1];
+    }
+    if (TYPE == 0) {
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j)
+            if ((uint32_t)j + 1 == B && best <= H[j]) { best = H[j]; bx = M + B - 1; by = M; }
+    } else if (TYPE == 2) {
+        const uint32_t m = min(M + B - 1, N) - (M - 1u);
+#pragma unroll
+        for (int j = 0; j < BMAX; ++j)
+            if ((uint32_t)j < B && (j == 0 || (uint32_t)j < m) && best <= H[j]) { best = H[j]; bx = M + j; by = M; }
+    }
+    A.score[k] = best;
+    snk[0] = bx; snk[1] = by;
+    if (bx == 0xFFFFFFFFu || by == 0xFFFFFFFFu) return;
+    const uint8_t *dir = reinterpret_cast<const uint8_t *>(A.dir);
+    uint8_t *out = A.ops + (size_t)k * A.ops_stride;
+    int32_t e = (int32_t)(bx - by), row = (int32_t)by - 1;
+    int state = 0;   // H / E / F
+    uint32_t cnt = 0;
+    bool found = false;
+    while (row >= 0) {
+        const uint8_t op = dir[(((size_t)row * A.words + (uint32_t)e / 4) * n + k) * 4 + ((uint32_t)e & 3u)];
+        if constexpr (GOTOH) {
+            const uint8_t h_op = op & 3u;
+            if (TYPE == 1 && state == 0 && h_op == SNK) { found = true; break; }
+            if (state == 1) {
+                if ((op & INS_EXT) == 0) state = 0;
+                --e; out[cnt++] = DEL;
+            } else if (state == 2) {
+                if ((op & DEL_EXT) == 0) state = 0;
+                ++e; --row; out[cnt++] = INS;
+            } else if (h_op == DEL) {
+                state = 1;
+            } else if (h_op == INS) {
+                state = 2;
+            } else {
+                --row; out[cnt++] = SUB;
+            }
+        } else {
+            if (op == DEL) { --e; out[cnt++] = DEL; }
+            else if (op == INS) { ++e; --row; out[cnt++] = INS; }
+            else { --row; out[cnt++] = SUB; }
+        }
+    }
+    const uint32_t sy = found ? (uint32_t)row + 1 : 0u;
+    src[0] = (uint32_t)e + sy; src[1] = sy;
+    A.n_ops[k] = cnt;
 }
 
 }  // namespace gx

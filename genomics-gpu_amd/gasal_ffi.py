@@ -35,6 +35,7 @@ EXPORTS = (
     "gasalx_nv_score_device", "gasalx_nv_score_host", "gasalx_nv_describe_plan",
     "gasalx_nv_banded_score_device", "gasalx_nv_banded_score_host",
     "gasalx_nv_traceback_device", "gasalx_nv_traceback_host",
+    "gasalx_nv_banded_traceback_device", "gasalx_nv_banded_traceback_host",
     "gasalx_multi_create", "gasalx_multi_destroy", "gasalx_multi_info", "gasalx_multi_engine",
     "gasalx_shard_bounds", "gasalx_multi_align_host", "gasalx_multi_pairhmm_host",
     "gasalx_multi_pairhmm_quals_host", "gasalx_multi_allgather", "gasalx_packed_pairs",
@@ -422,6 +423,40 @@ class Engine:
                                                 ctypes.c_uint32(max_text_len), v("score"), v("source"), v("sink"),
                                                 v("ops"), ctypes.c_uint32(ops_stride), v("n_ops"),
                                                 ctypes.c_void_p(stream or None)), "nv_traceback_device")
+
+    def nv_banded_traceback_host(self, aligner: "NvAligner", band: int, patterns: "PackedSet", texts: "PackedSet"):
+        """nvbio BatchedBandedAlignmentTraceback<band> (gasalx_nv_banded_traceback_host): the dict
+        oracle.nv_banded_traceback returns."""
+        n = patterns.n
+        po = np.asarray(patterns.offsets, np.int64)
+        stride = 2 * int((po[1:] - po[:-1]).max(initial=0)) + int(band)
+        sc = np.zeros(n, np.int32)
+        src = np.zeros(2 * n, np.uint32)
+        snk = np.zeros(2 * n, np.uint32)
+        ops = np.zeros(max(n * stride, 1), np.uint8)
+        nops = np.zeros(n, np.uint32)
+        ca = aligner.cstruct()
+        _check(lib().gasalx_nv_banded_traceback_host(self._h, ctypes.byref(ca), ctypes.c_uint32(band), ctypes.c_uint32(n),
+                                                     ctypes.byref(patterns.cstruct()), ctypes.c_uint64(len(patterns.words)),
+                                                     ctypes.byref(texts.cstruct()), ctypes.c_uint64(len(texts.words)),
+                                                     _p(sc), _p(src), _p(snk), _p(ops), ctypes.c_uint32(stride), _p(nops)),
+               "nv_banded_traceback_host")
+        return dict(score=sc, source=src.reshape(n, 2), sink=snk.reshape(n, 2),
+                    ops=[ops[k * stride:k * stride + int(nops[k])].copy() for k in range(n)])
+
+    def nv_banded_traceback_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
+                                        outs: dict, ops_stride: int, max_pattern_len: int = 0, stream: int = 0):
+        """Device-resident banded traceback (gasalx_nv_banded_traceback_device); arguments as
+        nv_traceback_device_ptrs."""
+        mk = lambda d: CNvStrings(d["words"], d.get("offsets") or None, d.get("length", 0), d["bits"],
+                                  int(d.get("big_endian", False)))
+        ca = aligner.cstruct()
+        v = lambda k: ctypes.c_void_p(outs[k] or None)
+        _check(lib().gasalx_nv_banded_traceback_device(self._h, ctypes.byref(ca), ctypes.c_uint32(band), ctypes.c_uint32(n),
+                                                       ctypes.byref(mk(pat)), ctypes.byref(mk(txt)),
+                                                       ctypes.c_uint32(max_pattern_len), v("score"), v("source"),
+                                                       v("sink"), v("ops"), ctypes.c_uint32(ops_stride), v("n_ops"),
+                                                       ctypes.c_void_p(stream or None)), "nv_banded_traceback_device")
 
     def nv_banded_score_device_ptrs(self, aligner: "NvAligner", band: int, n: int, pat: dict, txt: dict,
                                     scores_ptr: int, stream: int = 0, max_pattern_len: int = 0):

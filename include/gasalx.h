@@ -284,8 +284,9 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *ali
                                 const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores);
 
 /* nvbio's BatchedAlignmentTraceback<CHECKPOINTS> (NvB/nvbio/alignment/batched.h:436,
- * batched_inl.h:612-664, alignment_inl.h:365-465): the full-DP traceback of the Gotoh and
- * Smith-Waterman aligners (GASALX_NV_GOTOH / _SW; edit distance is not offered), GLOBAL / LOCAL /
+ * batched_inl.h:612-664, alignment_inl.h:365-465): the full-DP traceback of the Gotoh,
+ * Smith-Waterman and edit-distance aligners (ED runs as SW with 0 / -1 / -1 / -1, as
+ * ed/ed_inl.h:347-365 does), GLOBAL / LOCAL /
  * SEMI_GLOBAL, one pair per thread.  Per pair: the BestSink score, the Alignment's source and
  * sink as (x, y) = (text, pattern) coordinates in sources[2k..] / sinks[2k..] (0xFFFFFFFF when no
  * cell was reported), and the backtracker's pushes in push order (end of the alignment first) at
@@ -305,6 +306,24 @@ int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *aligne
                              const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores,
                              uint32_t *sources, uint32_t *sinks, uint8_t *ops, uint32_t ops_stride,
                              uint32_t *n_ops);
+/* nvbio BatchedBandedAlignmentTraceback<BAND_LEN, CHECKPOINTS, stream> (NvB/nvbio/alignment/
+ * batched.h:464-478, batched_banded_inl.h:248-297; nvBowtie's callers traceback_inl.h:239-257):
+ * the banded traceback of every pair, band length 2..32 as an argument.  Outputs as
+ * gasalx_nv_traceback_*: the BestSink score, source and sink (x = text, y = pattern end) and the
+ * pushes in push order; INT32_MIN and (-1, -1) ends for a pair whose text is shorter than its
+ * pattern.  ED, SW and Gotoh aligners.  ops_stride >= 2 x max pattern + band; nvbio's int16
+ * checkpoints bound (max pattern + band + 3) * max |score| <= 32736.  Workspace: max pattern x
+ * pad4(band) bytes per pair, held by the engine.  max_pattern_len 0 = read back. */
+int gasalx_nv_banded_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band,
+                                      uint32_t n_pairs, const gasalx_nv_strings *dev_patterns,
+                                      const gasalx_nv_strings *dev_texts, uint32_t max_pattern_len,
+                                      int32_t *dev_scores, uint32_t *dev_sources, uint32_t *dev_sinks,
+                                      uint8_t *dev_ops, uint32_t ops_stride, uint32_t *dev_n_ops, void *stream);
+int gasalx_nv_banded_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band,
+                                    uint32_t n_pairs, const gasalx_nv_strings *patterns, uint64_t pattern_words,
+                                    const gasalx_nv_strings *texts, uint64_t text_words, int32_t *scores,
+                                    uint32_t *sources, uint32_t *sinks, uint8_t *ops, uint32_t ops_stride,
+                                    uint32_t *n_ops);
 
 /* Multi-GPU from one host process.  A group holds one engine per
  * entry of a device list (entries may repeat a device); a host batch is split into

@@ -107,7 +107,7 @@ int orc_nv_banded_score_batch(int aligner, int type, const int32_t prm[6], uint3
                               const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
                               const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
                               int32_t *scores, int n_threads);
-/* nvbio full-DP traceback (nvbio_oracle.c): Gotoh and Smith-Waterman aligners */
+/* nvbio full-DP traceback (nvbio_oracle.c): Gotoh, Smith-Waterman and ED (= SW with 0/-1/-1/-1) */
 int32_t orc_nv_traceback_one(int aligner, int type, const int32_t prm[6], const uint32_t *pat, uint32_t M,
                              const uint32_t *txt, uint32_t N, uint32_t src[2], uint32_t snk[2], uint8_t *ops,
                              uint32_t *n_ops);
@@ -116,6 +116,16 @@ int orc_nv_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t
                            const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits, uint32_t tbig,
                            int32_t *scores, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
                            uint32_t *n_ops, int n_threads);
+/* nvbio banded traceback (BatchedBandedAlignmentTraceback<band>): per pair the BestSink score,
+ * source / sink (x = text, y = pattern) and the pushes; ED, SW and Gotoh aligners */
+int32_t orc_nv_banded_traceback_one(int aligner, int type, const int32_t prm[6], uint32_t band, const uint32_t *pat,
+                                    uint32_t M, const uint32_t *txt, uint32_t N, uint32_t src[2], uint32_t snk[2],
+                                    uint8_t *ops, uint32_t *n_ops);
+int orc_nv_banded_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t band, uint32_t n,
+                                  const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                                  const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits,
+                                  uint32_t tbig, int32_t *scores, uint32_t *src, uint32_t *snk, uint8_t *ops,
+                                  uint32_t ops_stride, uint32_t *n_ops, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -290,6 +290,10 @@ int32_t orc_nv_traceback_one(int aligner, int type, const int32_t prm[6], const 
     *n_ops = 0;
     src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
     if (M == 0 || N == 0) return INT32_MIN;
+    if (aligner == ORC_NV_ED) {   /* ed/ed_inl.h:347-365: SW with EditDistanceSWScheme (ed_utils.h:45-52) */
+        const int32_t ed[6] = {0, -1, 0, 0, -1, -1};
+        return orc_nv_traceback_one(ORC_NV_SW, type, ed, pat, M, txt, N, src, snk, ops, n_ops);
+    }
     uint8_t *dir = (uint8_t *)malloc((size_t)M * N);
     int32_t *Hp = (int32_t *)malloc((M + 1) * sizeof(int32_t));   /* H(i-1, c), c = -1 .. M-1 at [c + 1] */
     int32_t *Fp = (int32_t *)malloc((M + 1) * sizeof(int32_t));   /* F(i-1, c) at [c + 1] */
@@ -396,7 +400,6 @@ int orc_nv_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t
                            int32_t *scores, uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride,
                            uint32_t *n_ops, int n_threads) {
     if (!prm || !pw || !poff || !tw || !scores || !src || !snk || !ops || !n_ops) return -1;
-    if (aligner != ORC_NV_GOTOH && aligner != ORC_NV_SW) return -2;
 #ifdef _OPENMP
     if (n_threads <= 0) n_threads = omp_get_max_threads();
 #pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads)
@@ -413,6 +416,208 @@ int orc_nv_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t
                         ? orc_nv_traceback_one(aligner, type, prm, p, M, t, N, src + 2 * k, snk + 2 * k,
                                                ops + (size_t)k * ops_stride, n_ops + k)
                         : INT32_MIN;
+        free(p);
+        free(t);
+    }
+    return 0;
+}
+
+/*
+ * Banded traceback, one pair (nvbio banded_alignment_traceback, banded_inl.h:352-427, as
+ * BatchedBandedAlignmentTraceback<BAND_LEN, CHECKPOINTS> runs it, batched_banded_inl.h:248-297):
+ * the checkpoint pass with a BestSink, then the walk from its sink back through the recomputed
+ * band submatrices, then the clips.  Rows i = pattern symbols, band entry j = text symbol i + j
+ * (the orientation of the banded score, orc_nv_banded_score_one):
+ *   gotoh/gotoh_banded_inl.h:482-614  the row: j = 0 top (F) and diagonal; 0 < j < B-1 max3;
+ *       j = B-1 left (E) and diagonal; F from the row above is an INSERTION (pattern symbol
+ *       against a gap), E along the row a DELETION; hdir = top > left ? (top > diag ? INS : SUB)
+ *       : (left > diag ? DEL : SUB) (j = 0: top > diag ? INS : SUB; j = B-1: left > diag ? DEL :
+ *       SUB); fdir = F[j+1] + Ge > H[j+1] + Go ? DELETION_EXT; the E flag of cell j is the edir
+ *       of cell j-1's update (INSERTION_EXT when E + Ge > H + Go; SUB for j <= 1);
+ *   gotoh_banded_inl.h:323-339  stored flag: (LOCAL and H == 0 ? SINK : hdir) | edir | fdir;
+ *   gotoh_banded_inl.h:895-962  the walk: entry = sink.x - sink.y, row = sink.y - 1; H state:
+ *       DEL -> E state, INS -> F state, else row - 1 and push SUB; E state: entry - 1, push
+ *       DELETION, leave on a clear INSERTION_EXT bit; F state: entry + 1, row - 1, push INSERTION,
+ *       leave on a clear DELETION_EXT bit; LOCAL stops on SINK in the H state with source
+ *       (entry + row + 1, row + 1); otherwise the walk ends past row 0 with source (entry, 0);
+ *   sw/sw_banded_inl.h:392-475, 268-279, 740-798  the same for linear gaps (top + deletion,
+ *       left + insertion); the SW submatrix stores hdir as is, never SINK, so the SW walk runs
+ *       to row 0 in LOCAL too; ED is SW with EditDistanceSWScheme (ed_banded_inl.h:175-295);
+ *   the sink (banded score pass): LOCAL every cell (i + j + 1, i + 1) in row-then-band order,
+ *       SEMI_GLOBAL the last row's entries j < min(M + B - 1, N) - (M - 1) at (M + j, M),
+ *       GLOBAL entry B-1 at (M + B - 1, M); BestSink keeps the last maximum (sink_inl.h:59-68).
+ * nvbio recomputes each submatrix from int16 checkpoints clamped at -32736
+ * (gotoh_banded_inl.h:234-239): the same flags while every score stays above it, which the
+ * C-ABI's range condition ensures.  A pair with N < M keeps the BestSink's INT32_MIN and
+ * (-1, -1) ends (gotoh_banded_inl.h:431-432, banded_inl.h:389-392).
+ */
+int32_t orc_nv_banded_traceback_one(int aligner, int type, const int32_t prm[6], uint32_t band, const uint32_t *pat,
+                                    uint32_t M, const uint32_t *txt, uint32_t N, uint32_t src[2], uint32_t snk[2],
+                                    uint8_t *ops, uint32_t *n_ops) {
+    int32_t match = prm[0], mismatch = prm[1], Go = prm[2], Ge = prm[3], Del = prm[4], Ins = prm[5];
+    if (aligner == ORC_NV_ED) { match = 0; mismatch = -1; Del = -1; Ins = -1; }
+    enum { SUB = 0, INS = 1, DEL = 2, SNK = 3, INS_EXT = 4, DEL_EXT = 8 };
+    const int gotoh = aligner == ORC_NV_GOTOH;
+    *n_ops = 0;
+    src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
+    if (N < M || band < 2) return INT32_MIN;
+    const uint32_t B = band;
+    const int32_t infimum = -32768 - (Go > Ge ? Go : Ge);
+    int32_t *H = (int32_t *)malloc(B * sizeof(int32_t)), *F = (int32_t *)malloc(B * sizeof(int32_t));
+    uint8_t *dir = (uint8_t *)malloc((size_t)M * B + 1);
+    for (uint32_t j = 0; j < B; j++) {
+        if (gotoh) H[j] = j == 0 ? 0 : (type == ORC_NV_GLOBAL ? Go + (int32_t)(j - 1) * Ge : 0);
+        else H[j] = type == ORC_NV_GLOBAL ? (int32_t)j * Del : 0;
+        F[j] = infimum;
+    }
+    int32_t best = INT32_MIN;
+    uint32_t bx = 0xFFFFFFFFu, by = 0xFFFFFFFFu;
+#define TXT(k) ((k) < N ? txt[k] : 255u)
+#define REPORT(h, x, y) do { if (best <= (h)) { best = (h); bx = (x); by = (y); } } while (0)
+    for (uint32_t i = 0; i < M; i++) {
+        const uint32_t q = pat[i];
+        uint8_t *d = dir + (size_t)i * B;
+        if (gotoh) {
+            int32_t E = 0;
+            uint8_t edir = SUB;
+            for (uint32_t j = 0; j < B; j++) {
+                const int32_t diag = H[j] + (TXT(i + j) == q ? match : mismatch);
+                uint8_t fdir = SUB, hdir;
+                int32_t hi;
+                if (j + 1 < B) {
+                    const int32_t ftop = F[j + 1] + Ge, htop = H[j + 1] + Go;
+                    F[j] = nmax(ftop, htop);
+                    fdir = ftop > htop ? DEL_EXT : SUB;
+                } else {
+                    F[j] = infimum;
+                }
+                if (j == 0) {
+                    hi = nmax(F[0], diag);
+                    hdir = F[0] > diag ? INS : SUB;
+                } else if (j + 1 < B) {
+                    hi = nmax(nmax(F[j], E), diag);
+                    hdir = F[j] > E ? (F[j] > diag ? INS : SUB) : (E > diag ? DEL : SUB);
+                } else {
+                    hi = nmax(E, diag);
+                    hdir = E > diag ? DEL : SUB;
+                }
+                if (type == ORC_NV_LOCAL) {
+                    hi = nmax(hi, 0);
+                    if (hi == 0) hdir = SNK;
+                    REPORT(hi, i + j + 1, i + 1);
+                }
+                d[j] = (uint8_t)(hdir | (j == 0 ? SUB : edir) | fdir);
+                H[j] = hi;
+                if (j == 0) { E = hi + Go; edir = SUB; }
+                else {
+                    const int32_t eleft = E + Ge, ediag = hi + Go;
+                    edir = eleft > ediag ? INS_EXT : SUB;
+                    E = nmax(ediag, eleft);
+                }
+            }
+        } else {
+            for (uint32_t j = 0; j < B; j++) {
+                const int32_t diag = H[j] + (TXT(i + j) == q ? match : mismatch);
+                int32_t hi;
+                uint8_t hdir;
+                if (j == 0) {
+                    const int32_t top = H[1] + Del;
+                    hi = nmax(top, diag);
+                    hdir = top > diag ? INS : SUB;
+                } else if (j + 1 < B) {
+                    const int32_t top = H[j + 1] + Del, left = H[j - 1] + Ins;
+                    hi = nmax(nmax(top, left), diag);
+                    hdir = top > left ? (top > diag ? INS : SUB) : (left > diag ? DEL : SUB);
+                } else {
+                    const int32_t left = H[j - 1] + Ins;
+                    hi = nmax(left, diag);
+                    hdir = left > diag ? DEL : SUB;
+                }
+                if (type == ORC_NV_LOCAL) {
+                    hi = nmax(hi, 0);
+                    REPORT(hi, i + j + 1, i + 1);
+                }
+                d[j] = hdir;
+                H[j] = hi;
+            }
+        }
+    }
+    if (type == ORC_NV_GLOBAL) {
+        REPORT(H[B - 1], M + B - 1, M);
+    } else if (type == ORC_NV_SEMI_GLOBAL) {
+        const uint32_t m = (M + B - 1 < N ? M + B - 1 : N) - (M - 1u);
+        REPORT(H[0], M, M);
+        for (uint32_t j = 1; j < B; j++)
+            if (j < m) REPORT(H[j], M + j, M);
+    }
+#undef REPORT
+#undef TXT
+    snk[0] = bx; snk[1] = by;
+    uint32_t k = 0;
+    if (bx != 0xFFFFFFFFu && by != 0xFFFFFFFFu) {
+        int32_t e = (int32_t)bx - (int32_t)by, row = (int32_t)by - 1;
+        int state = 0;   /* H / E / F */
+        uint32_t sx = 0, sy = 0;
+        int found = 0;
+        while (row >= 0) {
+            const uint8_t op = dir[(size_t)row * B + (uint32_t)e];
+            if (gotoh) {
+                if (type == ORC_NV_LOCAL && state == 0 && (op & 3u) == SNK) { found = 1; break; }
+                if (state == 1) {
+                    if ((op & INS_EXT) == 0) state = 0;
+                    --e; ops[k++] = DEL;
+                } else if (state == 2) {
+                    if ((op & DEL_EXT) == 0) state = 0;
+                    ++e; --row; ops[k++] = INS;
+                } else if ((op & 3u) == DEL) {
+                    state = 1;
+                } else if ((op & 3u) == INS) {
+                    state = 2;
+                } else {
+                    --row; ops[k++] = SUB;
+                }
+            } else {
+                if (op == DEL) { --e; ops[k++] = DEL; }
+                else if (op == INS) { ++e; --row; ops[k++] = INS; }
+                else { --row; ops[k++] = SUB; }
+            }
+        }
+        if (found) { sy = (uint32_t)row + 1; sx = (uint32_t)e + sy; }
+        else { sy = 0; sx = (uint32_t)e; }
+        src[0] = sx; src[1] = sy;
+    }
+    *n_ops = k;
+    free(H); free(F); free(dir);
+    return best;
+}
+
+/* n pairs; ops of pair k at ops + k * ops_stride (ops_stride >= 2 M_k + band: every row is one
+ * SUB or INS push, and the DEL pushes are at most band - 1 plus the INS pushes) */
+int orc_nv_banded_traceback_batch(int aligner, int type, const int32_t prm[6], uint32_t band, uint32_t n,
+                                  const uint32_t *pw, const uint32_t *poff, uint32_t pbits, uint32_t pbig,
+                                  const uint32_t *tw, const uint32_t *toff, uint32_t tlen0, uint32_t tbits,
+                                  uint32_t tbig, int32_t *scores, uint32_t *src, uint32_t *snk, uint8_t *ops,
+                                  uint32_t ops_stride, uint32_t *n_ops, int n_threads) {
+    if (!prm || !pw || !poff || !tw || !scores || !src || !snk || !ops || !n_ops) return -1;
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(n_threads)
+#endif
+    for (long k = 0; k < (long)n; k++) {
+        const uint32_t M = poff[k + 1] - poff[k];
+        const uint64_t t0 = toff ? toff[k] : 0;
+        const uint32_t N = toff ? toff[k + 1] - toff[k] : tlen0;
+        uint32_t *p = (uint32_t *)malloc((M + 1) * sizeof(uint32_t));
+        uint32_t *t = (uint32_t *)malloc((N + 1) * sizeof(uint32_t));
+        for (uint32_t i = 0; i < M; i++) p[i] = nv_sym(pw, pbits, pbig, (uint64_t)poff[k] + i);
+        for (uint32_t i = 0; i < N; i++) t[i] = nv_sym(tw, tbits, tbig, t0 + i);
+        if (2 * M + band <= ops_stride) {
+            scores[k] = orc_nv_banded_traceback_one(aligner, type, prm, band, p, M, t, N, src + 2 * k, snk + 2 * k,
+                                                    ops + (size_t)k * ops_stride, n_ops + k);
+        } else {
+            scores[k] = INT32_MIN; n_ops[k] = 0;
+            src[2 * k] = src[2 * k + 1] = snk[2 * k] = snk[2 * k + 1] = 0xFFFFFFFFu;
+        }
         free(p);
         free(t);
     }

@@ -190,6 +190,31 @@ def nv_traceback(aligner, patterns, texts, n_threads=0):
                 ops=[ops[k * stride:k * stride + int(n_ops[k])].copy() for k in range(n)])
 
 
+def nv_banded_traceback(aligner, band, patterns, texts, n_threads=0):
+    """nvbio banded traceback restatement (nvbio_oracle.c orc_nv_banded_traceback_*):
+    BatchedBandedAlignmentTraceback<band>; the dict nv_traceback returns."""
+    n = len(patterns.offsets) - 1
+    po = np.asarray(patterns.offsets, np.int64)
+    plen = po[1:] - po[:-1]
+    stride = 2 * int(plen.max(initial=0)) + int(band) + 1
+    scores = np.zeros(n, np.int32)
+    src = np.zeros(2 * n, np.uint32)
+    snk = np.zeros(2 * n, np.uint32)
+    ops = np.zeros(max(n * stride, 1), np.uint8)
+    n_ops = np.zeros(n, np.uint32)
+    lib().orc_nv_banded_traceback_batch.restype = ctypes.c_int
+    rc = lib().orc_nv_banded_traceback_batch(
+        ctypes.c_int(aligner.aligner), ctypes.c_int(aligner.type), _ptr(aligner.prm()), ctypes.c_uint32(band),
+        ctypes.c_uint32(n), _ptr(patterns.words), _ptr(patterns.offsets), ctypes.c_uint32(patterns.bits),
+        ctypes.c_uint32(int(patterns.big_endian)), _ptr(texts.words), _ptr(texts.offsets),
+        ctypes.c_uint32(texts.length), ctypes.c_uint32(texts.bits), ctypes.c_uint32(int(texts.big_endian)),
+        _ptr(scores), _ptr(src), _ptr(snk), _ptr(ops), ctypes.c_uint32(stride), _ptr(n_ops), ctypes.c_int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"orc_nv_banded_traceback_batch failed ({rc})")
+    return dict(score=scores, source=src.reshape(n, 2), sink=snk.reshape(n, 2),
+                ops=[ops[k * stride:k * stride + int(n_ops[k])].copy() for k in range(n)])
+
+
 def nv_cigar_string(ops, M, source_y, sink_y):
     """nvbio-test's TestBacktracker string of one alignment, as rle() prints it: the pushes in
     push order, then the start clip (source.y 'S'; the end clip, pattern length - sink.y, is

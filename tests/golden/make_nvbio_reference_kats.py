@@ -15,6 +15,11 @@ nvbio unit test holds (NvB/nvbio-test/alignment_test.cu), restated as scores.
   banded traceback's CIGAR 4M1D3M and that its score equals ref_banded_sw's (:296-356): the
   banded optimum is the best score of that op string over the placements whose cells all
   lie inside the band (cell (i, c) in the band when 0 <= c - i < 7).
+* :796-826 runs the banded (band 31) Gotoh SEMI_GLOBAL traceback of a 150-symbol read against
+  a 181-symbol window (match 0, mismatch -5, gap open -8, gap extend -3) and asserts 147M2D3M;
+  :828-868 the full-DP Gotoh SEMI_GLOBAL traceback of a 144-symbol read against a 500-symbol
+  text (same scheme), 6I138M; :870-904 the full-DP edit-distance SEMI_GLOBAL traceback of the
+  same strings, 1I1M2I1M3I136M.  Their scores are implied the same way.
 * :680-745 holds banded (band 5) SEMI_GLOBAL edit-distance cases with stated scores.
   They are kept with the band; the test asserts them against the full-DP front-end where
   the full DP computes the same value (every case here: each optimum lies inside the band).
@@ -32,6 +37,22 @@ SCHEMES = {
     "sw": dict(match=2, mismatch=-1, deletion=-1, insertion=-1),           # :764-768
     "gotoh": dict(match=2, mismatch=-1, gap_open=-1, gap_ext=-1),          # :776-780
 }
+REAL_GOTOH = dict(match=0, mismatch=-5, gap_open=-8, gap_ext=-3)      # :813-817, :853-857
+ED_SCHEME = dict(match=0, mismatch=-1, deletion=-1, insertion=-1)      # ed_utils.h:45-52
+BANDED_READ = ("TTATGTAGGTGGTCTGGTTTTTGCCTTTTAAGCTTCTGCAAAAAACAACAACAAACTTGTGGTATTACACTGACTCTACAG"
+               "ATCAATTTGGGGACAACTTCCATGTGTTCCACCACCAATACTGAATCTTTCAATCGACTGACGTGGTAT")    # :810
+BANDED_WINDOW = ("ATCGGATTCTTTCTTACTTGTAGGTGGTCTGGTTTTTGCCTTTTAAGCTTCTGCAAAAAACAACAACAAACTTGTGGTATTA"
+                 "CACTGACTCTACAGATCAATTTGGGGACAACTTCCATGTGTTCCACCACCAATACTGAATCTTTCAATCGACTGACGTGGT"
+                 "ATCTCTCTCTCCATCTAT")                                                           # :811
+FULL_READ = ("TAGGAGGTAACATGTATGGAGCATTTACCATAGGCCAAGCACTGTTCTAAGAACTTCGGACATGTTATCTCACTTGTATAAG"
+             "TACTTAGGTGCCTACAACATAAGCAGCACCTGGTAAATTAAGTATTGAAAAAATGCAGATCG")          # :842-843
+FULL_TEXT = ("CAGCACTGACCGGTGAGCATAAACCCTGGGGATGCCCAGAGCTGGTACAGCCAGGAGCTCCAGAAGCGTGGGATTCTCAGAG"
+             "GGAAGTGGAGCTCACTGCTCTACAGGTCCTATTCAAGTTAGAAAGTAAGATACAATGCACACAAAGCCAAATTGTC"
+             "ATCATTCAGCTCCTATTACAGGGGAACTAAGAGCTGCATTGAAAATTATTTGCAAAGCTTGTAAGTGGTTCTGCCACTTAT"
+             "TAGCCGTGTGAACCTTAGCAAATTACCTAGCGTCTCTGAGTTTCAACTTCCTCATCTACAAAATAGAAATGATAATAAT"
+             "AACCGCATCGCAAGAGTTGTTGGAAAAATGAAAATGAGGTATCATAGGAGGTAACATGTATGGAGCATTTACCATAGGCC"
+             "AAGCACTGTTCTAAGAACTTCGGACATGTTATCTCACTTGTATAAGTACTTAGGTGCCTACAACATAAACAGCACCTGGT"
+             "AAATTAAGTATTGAAAAAATGC")                                                       # :844-848
 ED_CASES = [   # (test id, pattern, text, expected score): alignment_test.cu:680-745
     (1, "GGGTGCTCAA", "AAAAGGGTGCTCAA", 0),
     (2, "GGGTAAGCTC", "AAAAGGGTGCTCAA", -2),
@@ -84,15 +105,15 @@ def cigar_score(ops, p, t, start, kind, s):
     return total
 
 
-def implied(cigar, kind, type_):
+def implied(cigar, kind, type_, p=PATTERN, t=TEXT, scheme=None):
     ops = ops_of(cigar)[::-1]                   # printed sink to source
-    starts = [0] if type_ == "GLOBAL" else range(len(TEXT))
+    starts = [0] if type_ == "GLOBAL" else range(len(t))
     best = None
     for st in starts:
-        sc = cigar_score(ops, PATTERN, TEXT, st, kind, SCHEMES[kind])
+        sc = cigar_score(ops, p, t, st, kind, scheme or SCHEMES[kind])
         if sc is None:
             continue
-        if type_ == "GLOBAL" and st + sum(op != "I" for op in ops) != len(TEXT):
+        if type_ == "GLOBAL" and st + sum(op != "I" for op in ops) != len(t):
             continue
         best = sc if best is None or sc > best else best
     return best
@@ -117,11 +138,11 @@ def in_band_placements(ops, band):
     return out
 
 
-def implied_banded(cigar, kind, band):
+def implied_banded(cigar, kind, band, p=PATTERN, t=TEXT, scheme=None):
     ops = ops_of(cigar)[::-1]
     best = None
     for st in in_band_placements(ops, band):
-        sc = cigar_score(ops, PATTERN, TEXT, st, kind, SCHEMES[kind])
+        sc = cigar_score(ops, p, t, st, kind, scheme or SCHEMES[kind])
         if sc is not None:
             best = sc if best is None or sc > best else best
     return best
@@ -139,8 +160,20 @@ def main():
     banded = [dict(aligner="gotoh", type="SEMI_GLOBAL", band=7, scheme=SCHEMES["gotoh"], pattern=PATTERN, text=TEXT,
                    cigar="4M1D3M", score=implied_banded("4M1D3M", "gotoh", 7),
                    source="NvB/nvbio-test/alignment_test.cu:790 (SingleTest::banded, :296-356)")]
-    json.dump({"alignment": cases, "edit_distance": ed, "banded": banded}, open(OUT, "w"), indent=1)
-    print(OUT, [(c["aligner"], c["type"], c["score"]) for c in cases + banded])
+    banded.append(dict(aligner="gotoh", type="SEMI_GLOBAL", band=31, scheme=REAL_GOTOH, pattern=BANDED_READ,
+                       text=BANDED_WINDOW, cigar="147M2D3M",
+                       score=implied_banded("147M2D3M", "gotoh", 31, BANDED_READ, BANDED_WINDOW, REAL_GOTOH),
+                       source="NvB/nvbio-test/alignment_test.cu:796-826"))
+    real = [dict(aligner="gotoh", type="SEMI_GLOBAL", scheme=REAL_GOTOH, pattern=FULL_READ, text=FULL_TEXT,
+                 cigar="6I138M", score=implied("6I138M", "gotoh", "SEMI_GLOBAL", FULL_READ, FULL_TEXT, REAL_GOTOH),
+                 source="NvB/nvbio-test/alignment_test.cu:828-868"),
+            dict(aligner="ed", type="SEMI_GLOBAL", scheme=ED_SCHEME, pattern=FULL_READ, text=FULL_TEXT,
+                 cigar="1I1M2I1M3I136M",
+                 score=implied("1I1M2I1M3I136M", "sw", "SEMI_GLOBAL", FULL_READ, FULL_TEXT, ED_SCHEME),
+                 source="NvB/nvbio-test/alignment_test.cu:870-904")]
+    json.dump({"alignment": cases, "edit_distance": ed, "banded": banded, "traceback_real": real},
+              open(OUT, "w"), indent=1)
+    print(OUT, [(c["aligner"], c["type"], c["score"]) for c in cases + banded + real])
 
 
 if __name__ == "__main__":

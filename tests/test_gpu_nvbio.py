@@ -308,10 +308,10 @@ def test_banded_reference_known_answers(engine):
         P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
         T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
         assert int(engine.nv_banded_score_host(G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL), 5, P, T)[0]) == c["score"], c
-    (c,) = kats["banded"]
-    P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
-    T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
-    assert int(engine.nv_banded_score_host(TN.ref_aligner(c), 7, P, T)[0]) == c["score"]
+    for c in kats["banded"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        assert int(engine.nv_banded_score_host(TN.ref_aligner(c), c["band"], P, T)[0]) == c["score"]
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 257, 4097])
@@ -394,10 +394,96 @@ def test_traceback_random_pairs(engine, aligner, type_):
 
 
 def test_traceback_rejects(engine):
-    # edit distance has no traceback here; scores beyond nvbio's int16 columns are refused
+    # scores beyond nvbio's int16 columns are refused
     P = G.PackedSet.pack([np.zeros(10, np.uint32)])
     T = G.PackedSet.pack([np.zeros(10, np.uint32)], bits=2, big_endian=False)
     with pytest.raises(Exception):
-        engine.nv_traceback_host(G.NvAligner(G.NV_ED, G.NV_GLOBAL), P, T)
-    with pytest.raises(Exception):
         engine.nv_traceback_host(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 2000, -1, -2, -1), P, T)
+
+
+def test_traceback_real_problems(engine):
+    # alignment_test.cu:828-904 through the HIP kernel: 6I138M (Gotoh) and 1I1M2I1M3I136M (ED)
+    import test_nvbio_oracle as TN
+    for c in TN._ref_kats()["traceback_real"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        g = _check_traceback(engine, TN.ref_aligner(c), P, T)
+        assert int(g["score"][0]) == c["score"]
+        assert O.nv_cigar_string(g["ops"][0], len(c["pattern"]), g["source"][0][1], g["sink"][0][1]) == c["cigar"]
+
+
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_traceback_edit_distance(engine, type_):
+    # ED traces back as SW with EditDistanceSWScheme (ed/ed_inl.h:347-365)
+    rng = np.random.default_rng(640 + type_)
+    pats, texts = [], []
+    for _ in range(1000):
+        m = int(rng.integers(1, 120))
+        p = rng.integers(0, 4, m)
+        t = np.concatenate([rng.integers(0, 4, int(rng.integers(0, 16))), p, rng.integers(0, 4, int(rng.integers(0, 16)))])
+        t[rng.random(len(t)) < 0.05] = rng.integers(0, 4)
+        pats.append(p); texts.append(t)
+    _check_traceback(engine, G.NvAligner(G.NV_ED, type_), G.PackedSet.pack(pats),
+                     G.PackedSet.pack(texts, bits=2, big_endian=False))
+
+
+# ---- BatchedBandedAlignmentTraceback (gasalx_nv_banded_traceback_*, nvtrace.hpp) ----
+def _check_banded_traceback(engine, al, band, P, T):
+    g = engine.nv_banded_traceback_host(al, band, P, T)
+    o = O.nv_banded_traceback(al, band, P, T)
+    assert np.array_equal(g["score"], o["score"]), (al, band)
+    assert np.array_equal(g["source"], o["source"]) and np.array_equal(g["sink"], o["sink"]), (al, band)
+    bad = [k for k in range(len(g["ops"])) if not np.array_equal(g["ops"][k], o["ops"][k])]
+    assert not bad, f"{len(bad)} pairs' pushes differ, first #{bad[0]} {al} band {band}"
+    return g
+
+
+def test_banded_traceback_reference_cigars(engine):
+    # alignment_test.cu:790-793 (band 7, 4M1D3M) and :796-826 (band 31, 147M2D3M)
+    import test_nvbio_oracle as TN
+    for c in TN._ref_kats()["banded"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        for shared in (True, False):
+            T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False, shared=shared)
+            g = _check_banded_traceback(engine, TN.ref_aligner(c), c["band"], P, T)
+            assert int(g["score"][0]) == c["score"]
+            got = O.nv_cigar_string(g["ops"][0], len(c["pattern"]), g["source"][0][1], g["sink"][0][1])
+            assert got == c["cigar"], got
+
+
+@pytest.mark.parametrize("aligner", [G.NV_ED, G.NV_SW, G.NV_GOTOH], ids=["ed", "sw", "gotoh"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_banded_traceback_random_pairs(engine, aligner, type_):
+    # reads against windows a little longer than them, every band class (8 / 16 / 32 registers)
+    # and band lengths inside each; texts shorter than the pattern (skipped), empty patterns, N
+    # pattern symbols; per-pair texts and one shared text
+    rng = np.random.default_rng(720 + 3 * aligner + type_)
+    al = (G.NvAligner(G.NV_GOTOH, type_, 2, -3, -5, -2) if aligner == G.NV_GOTOH
+          else G.NvAligner(G.NV_SW, type_, match=2, mismatch=-1, deletion=-2, insertion=-3) if aligner == G.NV_SW
+          else G.NvAligner(G.NV_ED, type_))
+    for band in (2, 3, 7, 8, 9, 15, 16, 17, 31, 32):
+        pats, texts = [], []
+        for k in range(600):
+            m = int(rng.integers(0, 160))
+            p = rng.integers(0, 4, m).astype(np.uint32)
+            t = np.concatenate([rng.integers(0, 4, int(rng.integers(0, band))), p,
+                                rng.integers(0, 4, band)])[: max(0, m + int(rng.integers(-2, band + 2)))].copy()
+            t[rng.random(len(t)) < 0.06] = rng.integers(0, 4)
+            if k % 9 == 4 and m:
+                p[int(rng.integers(0, m))] = 4   # N
+            pats.append(p); texts.append(t)
+        P = G.PackedSet.pack(pats, bits=4, big_endian=True)
+        _check_banded_traceback(engine, al, band, P, G.PackedSet.pack(texts, bits=2, big_endian=False))
+        if band in (7, 31):
+            _check_banded_traceback(engine, al, band, P, G.PackedSet.pack([texts[1]], bits=2, big_endian=False, shared=True))
+
+
+def test_banded_traceback_rejects(engine):
+    P = G.PackedSet.pack([np.zeros(10, np.uint32)])
+    T = G.PackedSet.pack([np.zeros(12, np.uint32)], bits=2, big_endian=False)
+    al = G.NvAligner(G.NV_GOTOH, G.NV_SEMI_GLOBAL, 2, -1, -2, -1)
+    for band in (1, 33):
+        with pytest.raises(RuntimeError, match="band length"):
+            engine.nv_banded_traceback_host(al, band, P, T)
+    with pytest.raises(Exception):
+        engine.nv_banded_traceback_host(G.NvAligner(G.NV_GOTOH, G.NV_GLOBAL, 3000, -1, -2, -1), 8, P, T)

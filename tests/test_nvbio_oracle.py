@@ -130,6 +130,8 @@ def _ref_kats():
 def ref_aligner(c):
     t = {"GLOBAL": G.NV_GLOBAL, "LOCAL": G.NV_LOCAL, "SEMI_GLOBAL": G.NV_SEMI_GLOBAL}[c["type"]]
     s = c["scheme"]
+    if c["aligner"] == "ed":
+        return G.NvAligner(G.NV_ED, t)
     if c["aligner"] == "sw":
         return G.NvAligner(G.NV_SW, t, match=s["match"], mismatch=s["mismatch"], deletion=s["deletion"],
                            insertion=s["insertion"])
@@ -224,12 +226,16 @@ def test_reference_banded_edit_distance_cases():
 
 
 def test_reference_banded_gotoh_case():
-    # alignment_test.cu:790: the band-7 Gotoh SEMI_GLOBAL run whose traceback is 4M1D3M; its
-    # score is that CIGAR's best in-band placement (make_nvbio_reference_kats.py)
-    (c,) = _ref_kats()["banded"]
-    P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
-    T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
-    assert int(O.nv_banded_score(ref_aligner(c), c["band"], P, T)[0]) == c["score"] == 10
+    # alignment_test.cu:790 and :796-826: the band-7 and band-31 Gotoh SEMI_GLOBAL runs whose
+    # tracebacks are 4M1D3M and 147M2D3M; their scores are those CIGARs' best in-band
+    # placements (make_nvbio_reference_kats.py)
+    cases = _ref_kats()["banded"]
+    assert [c["band"] for c in cases] == [7, 31]
+    for c in cases:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        assert int(O.nv_banded_score(ref_aligner(c), c["band"], P, T)[0]) == c["score"]
+    assert cases[0]["score"] == 10
 
 
 @pytest.mark.parametrize("aligner,s", [(G.NV_GOTOH, (2, -1, -2, -1, 0, 0)), (G.NV_SW, (2, -3, 0, 0, -2, -3)),
@@ -312,3 +318,95 @@ def test_traceback_is_an_optimal_path(aligner, type_):
     assert list(r["score"]) == list(O.nv_score(al, P, T))
     for k in range(len(pats)):
         assert _replay_score(al, pats[k], texts[k], r["ops"][k], r["source"][k], r["sink"][k]) == r["score"][k], k
+
+
+def test_traceback_real_problems():
+    # alignment_test.cu:828-904: the 144 x 500 Gotoh and edit-distance SEMI_GLOBAL tracebacks
+    # (6I138M, 1I1M2I1M3I136M); ED traces back as SW with EditDistanceSWScheme
+    cases = _ref_kats()["traceback_real"]
+    assert [c["aligner"] for c in cases] == ["gotoh", "ed"]
+    for c in cases:
+        al = ref_aligner(c)
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        r = O.nv_traceback(al, P, T)
+        assert int(r["score"][0]) == c["score"] == int(O.nv_score(al, P, T)[0]), c["cigar"]
+        got = O.nv_cigar_string(r["ops"][0], len(c["pattern"]), r["source"][0][1], r["sink"][0][1])
+        assert got == c["cigar"], got
+
+
+# ---- BatchedBandedAlignmentTraceback (orc_nv_banded_traceback_*) ----
+def test_banded_traceback_reference_cigars():
+    # alignment_test.cu:790-793 (band 7, 4M1D3M) and :796-826 (band 31, 147M2D3M)
+    for c in _ref_kats()["banded"]:
+        P = G.PackedSet.pack([G.dna_n_codes(c["pattern"])])
+        T = G.PackedSet.pack([G.ref2_codes(c["text"])], bits=2, big_endian=False)
+        r = O.nv_banded_traceback(ref_aligner(c), c["band"], P, T)
+        assert int(r["score"][0]) == c["score"]
+        got = O.nv_cigar_string(r["ops"][0], len(c["pattern"]), r["source"][0][1], r["sink"][0][1])
+        assert got == c["cigar"], (c["band"], got)
+
+
+def _banded_replay(al, band, p, t, ops, src, snk):
+    """The score of the pushes replayed from the source (TestBacktracker::score's idea): the
+    banded SW scores a pattern-only step (INSERTION) with the deletion penalty and a text-only
+    step with the insertion penalty (sw_banded_inl.h:392-475: top + deletion, left + insertion);
+    a GLOBAL source at text offset e > 0 starts from row zero's H[e] (sw_banded_inl.h:44-54,
+    gotoh_banded_inl.h:48-77); text symbols past the end are nvbio's 255, a mismatch."""
+    gotoh = al.aligner == G.NV_GOTOH
+    sw = (0, -1, -1, -1) if al.aligner == G.NV_ED else (al.match, al.mismatch, al.deletion, al.insertion)
+    match, mismatch = (al.match, al.mismatch) if gotoh else sw[:2]
+    e = int(src[0])
+    s = 0
+    if al.type == G.NV_GLOBAL and e:
+        s = al.gap_open + (e - 1) * al.gap_ext if gotoh else e * sw[2]
+    j, k, prev = int(src[1]), e, None
+    for op in ops[::-1]:
+        if op == 0:
+            s += match if k < len(t) and p[j] == t[k] else mismatch
+            j += 1; k += 1
+        elif op == 1:
+            s += (al.gap_ext if prev == 1 else al.gap_open) if gotoh else sw[2]
+            j += 1
+        else:
+            s += (al.gap_ext if prev == 2 else al.gap_open) if gotoh else sw[3]
+            k += 1
+        prev = op
+    assert (k, j) == (int(snk[0]), int(snk[1]))
+    assert 0 <= k - j < band
+    return s
+
+
+@pytest.mark.parametrize("aligner", [G.NV_ED, G.NV_SW, G.NV_GOTOH], ids=["ed", "sw", "gotoh"])
+@pytest.mark.parametrize("type_", [G.NV_GLOBAL, G.NV_LOCAL, G.NV_SEMI_GLOBAL], ids=["global", "local", "semi"])
+def test_banded_traceback_is_an_optimal_path(aligner, type_):
+    # random pairs and bands: the score is the banded score pass's, and the pushes replayed from
+    # the source reach the sink with it -- except the SW LOCAL walk, which nvbio runs past the
+    # zero cells to row 0 (the SW submatrix holds no SINK flags, sw_banded_inl.h:268-279, 776)
+    rng = np.random.default_rng(77 + 3 * aligner + type_)
+    al = (G.NvAligner(G.NV_GOTOH, type_, 2, -3, -5, -2) if aligner == G.NV_GOTOH
+          else G.NvAligner(G.NV_SW, type_, match=2, mismatch=-1, deletion=-2, insertion=-3) if aligner == G.NV_SW
+          else G.NvAligner(G.NV_ED, type_))
+    for band in (2, 3, 7, 8, 16, 31, 32):
+        pats, texts = [], []
+        for _ in range(40):
+            m = int(rng.integers(0, 50))
+            p = rng.integers(0, 4, m)
+            t = np.concatenate([rng.integers(0, 4, int(rng.integers(0, band))), p,
+                                rng.integers(0, 4, int(rng.integers(0, band)))])[: m + int(rng.integers(-2, band + 2))]
+            t = t.copy()
+            t[rng.random(len(t)) < 0.1] = rng.integers(0, 4)
+            pats.append(p); texts.append(t)
+        P = G.PackedSet.pack(pats, bits=2, big_endian=False)
+        T = G.PackedSet.pack(texts, bits=2, big_endian=False)
+        r = O.nv_banded_traceback(al, band, P, T)
+        assert list(r["score"]) == list(O.nv_banded_score(al, band, P, T)), band
+        for k in range(len(pats)):
+            if len(texts[k]) < len(pats[k]):
+                assert r["score"][k] == INT32_MIN and list(r["sink"][k]) == [0xFFFFFFFF] * 2 and len(r["ops"][k]) == 0
+                continue
+            if aligner != G.NV_GOTOH and type_ == G.NV_LOCAL:
+                continue
+            if r["sink"][k][0] == 0xFFFFFFFF:
+                continue
+            assert _banded_replay(al, band, pats[k], texts[k], r["ops"][k], r["source"][k], r["sink"][k]) == r["score"][k], (band, k)

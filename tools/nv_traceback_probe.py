@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Throughput of the nvbio BatchedAlignmentTraceback front-end (gasalx_nv_traceback_device,
-nvtrace.hpp) on MI355X: reads of 150 bp drawn from per-pair text windows of 150 + slack symbols
+"""Throughput of the nvbio BatchedAlignmentTraceback and BatchedBandedAlignmentTraceback
+front-ends (gasalx_nv_traceback_device / gasalx_nv_banded_traceback_device, nvtrace.hpp) on
+MI355X: reads of 150 bp drawn from per-pair text windows of 150 + slack symbols
 (4-bit big-endian patterns, 2-bit texts, the sw-benchmark packing), inputs resident in HBM, timed
 with HIP events around the device call; the first pairs' outputs are checked against
 oracle/nvbio_oracle.c (test infrastructure).  Prints one JSON line per aligner/type.
@@ -71,6 +72,38 @@ def main():
         print(json.dumps({"probe": "nv_traceback", "aligner": name, "pairs": n, "pattern": m, "text": m + slack,
                           "ms": round(ms, 3), "gcups": round(cells / ms / 1e6, 1), "checked": k, "mismatches": bad,
                           "kernel": "nv_traceback_kernel (one pair per thread, full DP + walk)"}), flush=True)
+    for band in (15, 31):
+        for name, al in (("gotoh_semi", G.NvAligner(G.NV_GOTOH, G.NV_SEMI_GLOBAL, 0, -5, -8, -3)),
+                         ("gotoh_local", G.NvAligner(G.NV_GOTOH, G.NV_LOCAL, 2, -1, -2, -1)),
+                         ("ed_semi", G.NvAligner(G.NV_ED, G.NV_SEMI_GLOBAL))):
+            bstride = 2 * m + band
+            call = lambda: eng.nv_banded_traceback_device_ptrs(al, band, n, pat, txt, outs, bstride, m, s)
+            for _ in range(2):
+                call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 5
+            e0.record(ts)
+            for _ in range(reps):
+                call()
+            e1.record(ts)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            k = 500
+            o = O.nv_banded_traceback(al, band, G.PackedSet.pack(list(pats[:k])),
+                                      G.PackedSet.pack(list(texts[:k]), bits=2, big_endian=False))
+            g_sc = outs_t["score"][:k].cpu().numpy()
+            g_ops = outs_t["ops"][:k * bstride].cpu().numpy().reshape(k, bstride)
+            g_n = outs_t["n_ops"][:k].cpu().numpy()
+            bad = int((g_sc != o["score"]).sum()) + sum(int(not np.array_equal(g_ops[i, :g_n[i]], o["ops"][i]))
+                                                        for i in range(k))
+            bcells = n * m * band
+            flag_bytes = n * m * ((band + 3) // 4) * 4
+            print(json.dumps({"probe": "nv_banded_traceback", "aligner": name, "band": band, "pairs": n, "pattern": m,
+                              "text": m + slack, "ms": round(ms, 3), "gcups": round(bcells / ms / 1e6, 1),
+                              "flag_store_GBps": round(flag_bytes / ms / 1e6, 1), "checked": k, "mismatches": bad,
+                              "kernel": "nv_banded_traceback_kernel (one pair per thread, band in registers + walk)"}),
+                  flush=True)
 
 
 if __name__ == "__main__":
