@@ -9,16 +9,20 @@
  *   make_{edit_distance,smith_waterman,gotoh}_aligner       alignment/alignment_base.h:180-330
  *   nvbio::aln::BatchedBandedAlignmentScore<BAND_LEN, stream, scheduler>
  *                                                           batched.h:337-352, batched_banded_inl.h:44-75
+ *   nvbio::aln::BatchedAlignmentTraceback<CHECKPOINTS, stream, scheduler>
+ *                                                           batched.h:436-449, batched_inl.h:612-664
+ *   nvbio::aln::BatchedBandedAlignmentTraceback<BAND_LEN, CHECKPOINTS, stream, scheduler>
+ *                                                           batched.h:464-478, batched_banded_inl.h:248-297
  *   sw-benchmark's AlignmentStream (reads 4-bit DNA_N big-endian, reference 2-bit,
  *   int16 scores)                                           NvB/sw-benchmark/sw-benchmark.cu:100-215
  * Every scheduler maps to the same MI355X kernel (nvbio.hpp: lane groups per pattern,
  * text in LDS; banded: nvbanded.hpp, one pair per thread with the band in registers);
  * there is no temporary storage, so max_temp_storage() is 0.  The TextBlockingTag /
  * PatternBlockingTag score semantics are provided (both give the same scores), full and
- * banded.  Traceback: BatchedAlignmentTraceback<CHECKPOINTS, stream_type> (batched.h:436) for
- * the Gotoh and Smith-Waterman aligners, full DP, over a TracebackStream (nvtrace.hpp: one
- * pair per thread, as the reference's DeviceThreadScheduler runs it); the banded traceback and
- * the warp variants are not provided.
+ * banded.  Traceback: BatchedAlignmentTraceback<CHECKPOINTS, stream_type> (full DP) and
+ * BatchedBandedAlignmentTraceback<BAND_LEN, CHECKPOINTS, stream_type> for the edit-distance,
+ * Smith-Waterman and Gotoh aligners over a TracebackStream (nvtrace.hpp: one pair per thread,
+ * as the reference's DeviceThreadScheduler runs it); the warp variants are not provided.
  *
  * Header-only C++ over the flat C-ABI (gasalx.h); link with -lgasal.
  */
@@ -300,6 +304,36 @@ struct BatchedAlignmentTraceback {
                                                   stream.m_ops_stride, stream.m_n_ops, hip_stream);
         if (rc != GASALX_OK) {
             fprintf(stderr, "BatchedAlignmentTraceback::enact: %s\n", gasalx_last_error());
+            exit(EXIT_FAILURE);
+        }
+    }
+};
+
+// Banded traceback (banded_inl.h:352-427): the band's cells (i, i + j), j < BAND_LEN (2..32);
+// ops_stride >= 2 x max pattern length + BAND_LEN.  nvBowtie runs BAND_LEN 3 / 7 / 15 / 31
+// (nvBowtie/bowtie2/cuda/traceback_inl.h:239-257).  CHECKPOINTS only sizes the reference's
+// storage; the flags of every cell live in the engine's workspace here.
+template <uint32 BAND_LEN, uint32 CHECKPOINTS, typename stream_type, typename scheduler_type = DeviceThreadScheduler>
+struct BatchedBandedAlignmentTraceback {
+    typedef stream_type input_stream_type;
+    typedef typename stream_type::aligner_type aligner_type;
+
+    static uint64 min_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+    static uint64 max_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+
+    void enact(stream_type stream, uint64 temp_size = 0u, uint8 *temp = NULL, void *hip_stream = NULL) {
+        (void)temp_size; (void)temp;
+        const gasalx_nv_aligner a = stream.aligner().c_aligner();
+        gasalx_nv_strings p = {stream.m_patterns, stream.m_offsets, 0, stream.m_pattern_bits,
+                               stream.m_pattern_big_endian};
+        gasalx_nv_strings t = {stream.m_text, stream.m_text_offsets, stream.m_text_len, stream.m_text_bits,
+                               stream.m_text_big_endian};
+        const int rc = gasalx_nv_banded_traceback_device(engine(), &a, BAND_LEN, stream.size(), &p, &t,
+                                                         stream.max_pattern_length(), stream.m_scores32,
+                                                         stream.m_sources, stream.m_sinks, stream.m_ops,
+                                                         stream.m_ops_stride, stream.m_n_ops, hip_stream);
+        if (rc != GASALX_OK) {
+            fprintf(stderr, "BatchedBandedAlignmentTraceback::enact: %s\n", gasalx_last_error());
             exit(EXIT_FAILURE);
         }
     }

@@ -478,6 +478,16 @@ def test_banded_traceback_random_pairs(engine, aligner, type_):
             _check_banded_traceback(engine, al, band, P, G.PackedSet.pack([texts[1]], bits=2, big_endian=False, shared=True))
 
 
+def test_traceback_cpp_client():
+    # tools/nvbio_traceback_test: BatchedAlignmentTraceback and BatchedBandedAlignmentTraceback of
+    # include/nvbio_batched.h from C++, replayed into a backtracker, against the strings
+    # alignment_test.cu asserts (:778-793, :825, :867, :903)
+    prog = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "nvbio_traceback_test")
+    r = subprocess.run([prog], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(" ok") == 10, r.stdout
+
+
 def test_banded_traceback_rejects(engine):
     P = G.PackedSet.pack([np.zeros(10, np.uint32)])
     T = G.PackedSet.pack([np.zeros(12, np.uint32)], bits=2, big_endian=False)
