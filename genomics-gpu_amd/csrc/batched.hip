@@ -354,7 +354,8 @@ int nv_traceback_device(const gasalx_nv_aligner &al, uint32_t n, const gasalx_nv
 
 // BatchedBandedAlignmentTraceback<band> (nvtrace.hpp nv_banded_traceback_kernel); ED runs as
 // SW with EditDistanceSWScheme (ed_banded_inl.h:175-295).  The band's register arrays come in
-// 8, 16 and 32 cells; the band length itself is a kernel argument.
+// 8, 16 and 32 cells with the band length as a kernel argument, and exactly 7, 15 and 31 cells
+// (nvBowtie's BAND_LEN values, traceback_inl.h:239-257) with the length folded in.
 int nv_banded_traceback_device(const gasalx_nv_aligner &al, uint32_t band, uint32_t n, const gasalx_nv_strings &pat,
                                const gasalx_nv_strings &txt, uint32_t max_p, uint32_t *dir, int32_t *score,
                                uint32_t *src, uint32_t *snk, uint8_t *ops, uint32_t ops_stride, uint32_t *n_ops,
@@ -386,8 +387,14 @@ int nv_banded_traceback_device(const gasalx_nv_aligner &al, uint32_t band, uint3
     static const Fn tab[2][3][3] = {{NVBT_ROW(false, 0), NVBT_ROW(false, 1), NVBT_ROW(false, 2)},
                                     {NVBT_ROW(true, 0), NVBT_ROW(true, 1), NVBT_ROW(true, 2)}};
 #undef NVBT_ROW
-    const int cls = band <= 8 ? 0 : band <= 16 ? 1 : 2;
-    hipLaunchKernelGGL(tab[al.aligner == NV_GOTOH ? 1 : 0][al.type][cls], dim3((n + 255) / 256), dim3(256), 0, st, A);
+#define NVBT_EX(G, T) {&nv_banded_traceback_kernel<G, T, 7, true>, &nv_banded_traceback_kernel<G, T, 15, true>, &nv_banded_traceback_kernel<G, T, 31, true>}
+    static const Fn tab_ex[2][3][3] = {{NVBT_EX(false, 0), NVBT_EX(false, 1), NVBT_EX(false, 2)},
+                                       {NVBT_EX(true, 0), NVBT_EX(true, 1), NVBT_EX(true, 2)}};
+#undef NVBT_EX
+    const int g = al.aligner == NV_GOTOH ? 1 : 0;
+    const int ex = band == 7 ? 0 : band == 15 ? 1 : band == 31 ? 2 : -1;
+    const Fn fn = ex >= 0 ? tab_ex[g][al.type][ex] : tab[g][al.type][band <= 8 ? 0 : band <= 16 ? 1 : 2];
+    hipLaunchKernelGGL(fn, dim3((n + 255) / 256), dim3(256), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_error(hipGetErrorString(e)); return GASALX_EDEVICE; }
     return GASALX_OK;

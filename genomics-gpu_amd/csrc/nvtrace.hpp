@@ -220,7 +220,9 @@ struct NvBandTbArgs {
     uint32_t *n_ops;
 };
 
-template <bool GOTOH, int TYPE, int BMAX>
+// EX: the band length is BMAX itself (nvBowtie's BAND_LEN 7 / 15 / 31 get their own code, as
+// nvbio's template argument does), so the per-cell band tests fold at compile time
+template <bool GOTOH, int TYPE, int BMAX, bool EX = false>
 __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= A.n) return;
@@ -228,7 +230,8 @@ __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A
     const uint32_t po = A.poff[k], M = A.poff[k + 1] - po;
     const bool shared = A.toff == nullptr;
     const uint32_t to = shared ? 0u : A.toff[k], N = shared ? A.tlen0 : A.toff[k + 1] - to;
-    const uint32_t B = A.band, n = A.n;
+    const uint32_t B = EX ? (uint32_t)BMAX : A.band, n = A.n;
+    const uint32_t words = EX ? (uint32_t)(BMAX + 3) / 4 : A.words;
     uint32_t *src = A.src + 2 * (size_t)k, *snk = A.snk + 2 * (size_t)k;
     src[0] = src[1] = snk[0] = snk[1] = 0xFFFFFFFFu;
     A.n_ops[k] = 0;
@@ -262,12 +265,12 @@ __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A
             if ((uint32_t)j + 1 == B) tc[j] = g_last;
         int32_t E = 0, hprev = 0;
         uint32_t edir = SUB;
-        uint32_t fw[BMAX / 4];
+        uint32_t fw[(BMAX + 3) / 4];
 #pragma unroll
-        for (int w = 0; w < BMAX / 4; ++w) fw[w] = 0;
+        for (int w = 0; w < (BMAX + 3) / 4; ++w) fw[w] = 0;
 #pragma unroll
         for (int j = 0; j < BMAX; ++j) {
-            if ((uint32_t)j >= B) break;
+            if ((uint32_t)j >= B) continue;   // (not break: the loop must unroll fully)
             const bool last = (uint32_t)j + 1 == B;
             const int jn = j + 1 < BMAX ? j + 1 : j;
             const int32_t diag = H[j] + (tc[j] == q ? S_eq : S_ne);
@@ -314,8 +317,8 @@ __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A
             fw[j / 4] |= d << (8 * (j % 4));
         }
 #pragma unroll
-        for (int w = 0; w < BMAX / 4; ++w)
-            if ((uint32_t)w < A.words) A.dir[((size_t)i * A.words + w) * n + k] = fw[w];
+        for (int w = 0; w < (BMAX + 3) / 4; ++w)
+            if ((uint32_t)w < words) A.dir[((size_t)i * words + w) * n + k] = fw[w];
 #pragma unroll
         for (int j = 0; j + 1 < BMAX; ++j)
             if ((uint32_t)j + 1 < B) tc[j] = tc[j + 1];
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A
     uint32_t cnt = 0;
     bool found = false;
     while (row >= 0) {
-        const uint8_t op = dir[(((size_t)row * A.words + (uint32_t)e / 4) * n + k) * 4 + ((uint32_t)e & 3u)];
+        const uint8_t op = dir[(((size_t)row * words + (uint32_t)e / 4) * n + k) * 4 + ((uint32_t)e & 3u)];
         if constexpr (GOTOH) {
             const uint8_t h_op = op & 3u;
             if (TYPE == 1 && state == 0 && h_op == SNK) { found = true; break; }
