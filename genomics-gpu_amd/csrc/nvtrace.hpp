@@ -51,6 +51,33 @@ __device__ __forceinline__ uint32_t nvtb_symbol(const uint32_t *w, uint32_t bits
     return (w[s / per] >> sh) & (bits == 32u ? 0xFFFFFFFFu : ((1u << bits) - 1u));
 }
 
+// The walk's pushes into a pair's output (ops + k * ops_stride, push order): single bytes until the
+// output reaches a 4-byte boundary, then one 32-bit store per 4 pushes.  A wave's byte stores each
+// touch 64 different lines; this issues a quarter of them (band 7: 0.67 -> 0.41 ms per 262 K pairs,
+// profiles/r05/nvbtb/).
+struct NvPushes {
+    uint8_t *out;
+    uint32_t a0, head, acc, cnt;
+    __device__ __forceinline__ explicit NvPushes(uint8_t *o)
+        : out(o), a0((uint32_t)(reinterpret_cast<uintptr_t>(o) & 3u)), head(0), acc(0), cnt(0) {
+        head = (4u - a0) & 3u;
+    }
+    __device__ __forceinline__ void push(uint32_t op) {
+        const uint32_t a = (a0 + cnt) & 3u;
+        if (cnt < head) {
+            out[cnt] = (uint8_t)op;
+        } else {
+            acc |= op << (8u * a);
+            if (a == 3u) { *reinterpret_cast<uint32_t *>(out + cnt - 3) = acc; acc = 0; }
+        }
+        ++cnt;
+    }
+    __device__ __forceinline__ void flush() {   // the pushes of the last, partial word
+        if (cnt > head)
+            for (uint32_t i = cnt - ((a0 + cnt) & 3u); i < cnt; ++i) out[i] = (uint8_t)(acc >> (8u * ((a0 + i) & 3u)));
+    }
+};
+
 // TYPE: 0 GLOBAL, 1 LOCAL, 2 SEMI_GLOBAL (nvbio AlignmentType).  The pass runs in stripes of 8
 // pattern columns, as the reference's PatternBlockingTag does: a stripe's H and F across its 8
 // columns stay in registers, the (H, E) of its last column goes to the next stripe through one
@@ -150,10 +177,9 @@ __global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
     auto dcell = [&](uint32_t i, uint32_t j) -> uint8_t {
         return dir[(((size_t)i * stripes + j / BAND) * n + k) * 8 + (j % BAND)];
     };
-    uint8_t *out = A.ops + (size_t)k * A.ops_stride;
+    NvPushes out(A.ops + (size_t)k * A.ops_stride);
     int32_t row = (int32_t)bx, col = (int32_t)by - 1;
     int state = 0;   // H / E / F
-    uint32_t cnt = 0;
     while (row > 0 && col >= 0) {
         const uint8_t op = dcell((uint32_t)(row - 1), (uint32_t)col);
         if constexpr (GOTOH) {
@@ -161,31 +187,32 @@ __global__ __launch_bounds__(256) void nv_traceback_kernel(NvTbArgs A) {
             if (TYPE == 1 && state == 0 && h_op == SNK) break;
             if (state == 1) {
                 if ((op & INS_EXT) == 0) state = 0;
-                --col; out[cnt++] = INS;
+                --col; out.push(INS);
             } else if (state == 2) {
                 if ((op & DEL_EXT) == 0) state = 0;
-                --row; out[cnt++] = DEL;
+                --row; out.push(DEL);
             } else if (h_op == INS) {
                 state = 1;
             } else if (h_op == DEL) {
                 state = 2;
             } else {
-                --col; --row; out[cnt++] = SUB;
+                --col; --row; out.push(SUB);
             }
         } else {
             if (TYPE == 1 && op == SNK) break;
             if (op != DEL) --col;
             if (op != INS) --row;
-            out[cnt++] = op;
+            out.push(op);
         }
     }
     uint32_t sx = (uint32_t)row, sy = (uint32_t)(col + 1);
     if (TYPE != 1 && sx == 0)
-        for (; sy > 0; --sy) out[cnt++] = INS;
+        for (; sy > 0; --sy) out.push(INS);
     if (TYPE == 0 && sy == 0)
-        for (; sx > 0; --sx) out[cnt++] = DEL;
+        for (; sx > 0; --sx) out.push(DEL);
+    out.flush();
     src[0] = sx; src[1] = sy;
-    A.n_ops[k] = cnt;
+    A.n_ops[k] = out.cnt;
     A.score[k] = best;
 }
 
@@ -336,39 +363,66 @@ __global__ __launch_bounds__(256) void nv_banded_traceback_kernel(NvBandTbArgs A
     A.score[k] = best;
     snk[0] = bx; snk[1] = by;
     if (bx == 0xFFFFFFFFu || by == 0xFFFFFFFFu) return;
-    const uint8_t *dir = reinterpret_cast<const uint8_t *>(A.dir);
-    uint8_t *out = A.ops + (size_t)k * A.ops_stride;
+    // The walk reads its flags P rows at a time: when any lane of the wave steps above the rows it
+    // holds, every active lane loads the P rows ending at its own row (P x words independent loads,
+    // one memory latency), so the wave waits on memory about once per P rows instead of once per
+    // step; the step's byte is picked from the held rows by selects.
+    constexpr int P = 8, WW = (BMAX + 3) / 4;
+    uint32_t held[P][WW];
+    NvPushes out(A.ops + (size_t)k * A.ops_stride);
     int32_t e = (int32_t)(bx - by), row = (int32_t)by - 1;
+    int32_t base = 0x7FFFFFFF;   // rows [base, base + P) held (none yet)
     int state = 0;   // H / E / F
-    uint32_t cnt = 0;
     bool found = false;
     while (row >= 0) {
-        const uint8_t op = dir[(((size_t)row * words + (uint32_t)e / 4) * n + k) * 4 + ((uint32_t)e & 3u)];
+        if (__any(row < base)) {
+            base = max(row - (P - 1), 0);
+#pragma unroll
+            for (int p = 0; p < P; ++p)
+#pragma unroll
+                for (int w = 0; w < WW; ++w)
+                    if ((uint32_t)w < words)
+                        held[p][w] = base + p <= row ? A.dir[((size_t)(base + p) * words + w) * n + k] : 0u;
+        }
+        const int32_t rr = row - base;
+        uint32_t rowv[WW];
+#pragma unroll
+        for (int w = 0; w < WW; ++w) {
+            rowv[w] = held[0][w];
+#pragma unroll
+            for (int p = 1; p < P; ++p) rowv[w] = rr == p ? held[p][w] : rowv[w];
+        }
+        const uint32_t wi = (uint32_t)e >> 2;
+        uint32_t word = rowv[0];
+#pragma unroll
+        for (int w = 1; w < WW; ++w) word = wi == (uint32_t)w ? rowv[w] : word;
+        const uint8_t op = (uint8_t)(word >> (8u * ((uint32_t)e & 3u)));
         if constexpr (GOTOH) {
             const uint8_t h_op = op & 3u;
             if (TYPE == 1 && state == 0 && h_op == SNK) { found = true; break; }
             if (state == 1) {
                 if ((op & INS_EXT) == 0) state = 0;
-                --e; out[cnt++] = DEL;
+                --e; out.push(DEL);
             } else if (state == 2) {
                 if ((op & DEL_EXT) == 0) state = 0;
-                ++e; --row; out[cnt++] = INS;
+                ++e; --row; out.push(INS);
             } else if (h_op == DEL) {
                 state = 1;
             } else if (h_op == INS) {
                 state = 2;
             } else {
-                --row; out[cnt++] = SUB;
+                --row; out.push(SUB);
             }
         } else {
-            if (op == DEL) { --e; out[cnt++] = DEL; }
-            else if (op == INS) { ++e; --row; out[cnt++] = INS; }
-            else { --row; out[cnt++] = SUB; }
+            if (op == DEL) { --e; out.push(DEL); }
+            else if (op == INS) { ++e; --row; out.push(INS); }
+            else { --row; out.push(SUB); }
         }
     }
+    out.flush();
     const uint32_t sy = found ? (uint32_t)row + 1 : 0u;
     src[0] = (uint32_t)e + sy; src[1] = sy;
-    A.n_ops[k] = cnt;
+    A.n_ops[k] = out.cnt;
 }
 
 }  // namespace gx
