@@ -143,7 +143,11 @@ def census(lib, sym, rates):
     nvalu = lambda g: max(1, sum(1 for _, x, _ in g if x.startswith("v_")))
     innermost = [g for g in loops if inner(g)] or loops
     with_dpp = [g for g in innermost if dpp(g) and arith(g) > 0]
-    pool = with_dpp or [g for g in innermost if arith(g) > 0] or innermost
+    pool = with_dpp or [g for g in innermost if arith(g) > 0]
+    if not pool:   # no loop carries the cell arithmetic (e.g. nv16_kernel): no steady loop to price
+        return {"kernel": sym, "loop_valu": None, "cycles_per_valu": None,
+                "note": "no innermost loop with packed or fp32 cell arithmetic: the steady loop is not "
+                        "identified, so no issue-priced figure", "rates": os.path.relpath(rates, ROOT)}
     seg = max(pool, key=lambda g: (arith(g) / nvalu(g), -len(g)))
     best = (0, seg)
     # static census: conditionally executed blocks (divergent captures, resets) are counted
