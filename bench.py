@@ -773,19 +773,24 @@ def main():
         for i in range(args.warmup):
             step(i)
     else:
-        # time-based: every rank warms for the same number of steps (the max over ranks)
+        # time-based: every rank runs the same steps.  Each step holds a collective (the score
+        # all-gather), so the decision to stop is taken together: after each step from the third
+        # on, the ranks all-reduce "keep warming" (MAX over ranks) and all leave at the same step
+        # (a per-rank decision could leave one rank in a step's all_gather while
+        # another had moved on to the next collective)
         i, t_w = 0, time.perf_counter()
-        while i < 3 or time.perf_counter() - t_w < args.warmup_seconds:
+        while True:
             step(i)
             i += 1
-            if i >= 3:
-                torch.cuda.synchronize(dev)
-        wt = torch.tensor([i], dtype=torch.int64, device=dev)
-        if world > 1:
-            wt = allreduce(wt, dist.ReduceOp.MAX)
-        while i < int(wt[0]):
-            step(i)
-            i += 1
+            if i < 3:
+                continue
+            torch.cuda.synchronize(dev)
+            keep = torch.tensor([1 if time.perf_counter() - t_w < args.warmup_seconds else 0],
+                                dtype=torch.int64, device=dev)
+            if world > 1:
+                keep = allreduce(keep, dist.ReduceOp.MAX)
+            if int(keep[0]) == 0:
+                break
         args.warmup = i
     torch.cuda.synchronize(dev)
     if world > 1:

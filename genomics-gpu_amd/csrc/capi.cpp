@@ -652,6 +652,20 @@ static int64_t nv_score_mag(const gasalx_nv_aligner *al) {
                               std::abs((int64_t)al->deletion), std::abs((int64_t)al->insertion), 1});
 }
 
+// nvbio traceback workspace per call (the engine's: flags of every cell, one DP row per pair) and
+// the chunk budget the device entry points split a batch by
+static constexpr uint64_t kNvTbBudget = 4ull << 30;
+uint64_t gasalx_nv_traceback_workspace(uint32_t max_p, uint32_t max_t, uint32_t n) {
+    const uint64_t per = (uint64_t)((max_p + 7) / 8) * 8 * max_t + (uint64_t)max_t * 8;
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kNvTbBudget / std::max<uint64_t>(per, 1)));
+    return per * chunk + 128;
+}
+uint64_t gasalx_nv_banded_traceback_workspace(uint32_t max_p, uint32_t band, uint32_t n) {
+    const uint64_t per = (uint64_t)max_p * ((band + 3) / 4) * 4;
+    const uint64_t chunk = std::max<uint64_t>(1, std::min<uint64_t>(n, kNvTbBudget / std::max<uint64_t>(per, 1)));
+    return per * chunk + 64;
+}
+
 static int nv_tb_checks(const gasalx_nv_aligner *al, uint32_t max_p, uint32_t max_t, uint32_t ops_stride) {
     const int64_t mag = nv_score_mag(al);
     if (((int64_t)max_p + max_t + 2) * mag > 32767) {
@@ -682,10 +696,23 @@ int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *al, 
     if (!txt->offsets) max_t = txt->length;
     int rc = nv_tb_checks(al, max_p, max_t, ops_stride);
     if (rc) return rc;
-    CK(eng->nv_dir.reserve((size_t)((max_p + 7) / 8) * 8 * max_t * n + 64));
-    CK(eng->nv_row.reserve((size_t)max_t * n * 8 + 64));
-    return gx::nv_traceback_device(*al, n, *pat, *txt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
-                                   scores, sources, sinks, ops, ops_stride, n_ops, st);
+    // the batch runs in chunks whose workspace (flags of every cell + one row per pair) stays
+    // within kNvTbBudget (1 M 150 x 182 pairs would otherwise take 28 GB of HBM)
+    const uint64_t per = gasalx_nv_traceback_workspace(max_p, max_t, 1);
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, kNvTbBudget / per));
+    CK(eng->nv_dir.reserve((size_t)((max_p + 7) / 8) * 8 * max_t * chunk + 64));
+    CK(eng->nv_row.reserve((size_t)max_t * chunk * 8 + 64));
+    for (uint32_t s = 0; s < n; s += chunk) {
+        const uint32_t m = std::min(chunk, n - s);
+        gasalx_nv_strings p = *pat, t = *txt;
+        p.offsets = pat->offsets + s;
+        if (txt->offsets) t.offsets = txt->offsets + s;
+        rc = gx::nv_traceback_device(*al, m, p, t, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
+                                     scores + s, sources + 2ull * s, sinks + 2ull * s, ops + (size_t)s * ops_stride,
+                                     ops_stride, n_ops + s, st);
+        if (rc) return rc;
+    }
+    return GASALX_OK;
 }
 
 int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t n, const gasalx_nv_strings *pat,
@@ -715,11 +742,9 @@ int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, ui
     CK(eng->nv_snk.reserve((size_t)n * 8));
     CK(eng->nv_ops.reserve((size_t)n * ops_stride + 64));
     CK(eng->nv_nops.reserve((size_t)n * 4));
-    CK(eng->nv_dir.reserve((size_t)((max_p + 7) / 8) * 8 * max_t * n + 64));
-    CK(eng->nv_row.reserve((size_t)max_t * n * 8 + 64));
-    rc = gx::nv_traceback_device(*al, n, dp, dt, max_p, max_t, eng->nv_dir.as<uint8_t>(), eng->nv_row.as<int32_t>(),
-                                 eng->nv_s.as<int32_t>(), eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(),
-                                 eng->nv_ops.as<uint8_t>(), ops_stride, eng->nv_nops.as<uint32_t>(), st);
+    rc = gasalx_nv_traceback_device(eng, al, n, &dp, &dt, max_p, max_t, eng->nv_s.as<int32_t>(),
+                                    eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(), eng->nv_ops.as<uint8_t>(),
+                                    ops_stride, eng->nv_nops.as<uint32_t>(), st);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(sources, eng->nv_src.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
@@ -761,9 +786,20 @@ int gasalx_nv_banded_traceback_device(gasalx_engine *eng, const gasalx_nv_aligne
     }
     int rc = nv_btb_checks(al, band, max_p, ops_stride);
     if (rc) return rc;
-    CK(eng->nv_dir.reserve((size_t)max_p * ((band + 3) / 4) * 4 * n + 64));
-    return gx::nv_banded_traceback_device(*al, band, n, *pat, *txt, max_p, eng->nv_dir.as<uint32_t>(), scores, sources,
-                                          sinks, ops, ops_stride, n_ops, st);
+    const uint64_t per = gasalx_nv_banded_traceback_workspace(max_p, band, 1);
+    const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n, kNvTbBudget / per));
+    CK(eng->nv_dir.reserve((size_t)max_p * ((band + 3) / 4) * 4 * chunk + 64));
+    for (uint32_t s = 0; s < n; s += chunk) {
+        const uint32_t m = std::min(chunk, n - s);
+        gasalx_nv_strings p = *pat, t = *txt;
+        p.offsets = pat->offsets + s;
+        if (txt->offsets) t.offsets = txt->offsets + s;
+        rc = gx::nv_banded_traceback_device(*al, band, m, p, t, max_p, eng->nv_dir.as<uint32_t>(), scores + s,
+                                            sources + 2ull * s, sinks + 2ull * s, ops + (size_t)s * ops_stride,
+                                            ops_stride, n_ops + s, st);
+        if (rc) return rc;
+    }
+    return GASALX_OK;
 }
 
 int gasalx_nv_banded_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *al, uint32_t band, uint32_t n,
@@ -793,10 +829,9 @@ int gasalx_nv_banded_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner 
     CK(eng->nv_snk.reserve((size_t)n * 8));
     CK(eng->nv_ops.reserve((size_t)n * ops_stride + 64));
     CK(eng->nv_nops.reserve((size_t)n * 4));
-    CK(eng->nv_dir.reserve((size_t)max_p * ((band + 3) / 4) * 4 * n + 64));
-    rc = gx::nv_banded_traceback_device(*al, band, n, dp, dt, max_p, eng->nv_dir.as<uint32_t>(), eng->nv_s.as<int32_t>(),
-                                        eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(), eng->nv_ops.as<uint8_t>(),
-                                        ops_stride, eng->nv_nops.as<uint32_t>(), st);
+    rc = gasalx_nv_banded_traceback_device(eng, al, band, n, &dp, &dt, max_p, eng->nv_s.as<int32_t>(),
+                                           eng->nv_src.as<uint32_t>(), eng->nv_snk.as<uint32_t>(),
+                                           eng->nv_ops.as<uint8_t>(), ops_stride, eng->nv_nops.as<uint32_t>(), st);
     if (rc) { (void)hipStreamSynchronize(st); return rc; }
     CK(hipMemcpyAsync(scores, eng->nv_s.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     CK(hipMemcpyAsync(sources, eng->nv_src.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));

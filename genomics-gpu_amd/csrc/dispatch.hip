@@ -669,6 +669,7 @@ static int start_reverse(Workspace &ws, int mode, const gasalx_params &p, const 
     A.qoff = b.q_offsets; A.toff = b.t_offsets; A.qlen = rqlen; A.tlen = rtlen;
     A.rev = 1;
     A.perm = perm;
+    A.perm_xkey = (mode == REV_SEMI || qkey) ? 1 : 0;   // sorted by the register-axis words first
     A.score = rscore; A.qend = rqend; A.tend = rtend;
     A.stop = mode == REV_SEMI ? score : nullptr;     // the forward score per pair
     A.lstop = lstop ? score : nullptr;
@@ -727,6 +728,10 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
     if (p.algo == 6 && !b.seed_scores) { set_error("KSW needs seed_scores"); return GASALX_EINVAL; }
     if (shape.max_q == 0 || shape.max_t == 0) { set_error("zero-length sequence"); return GASALX_ERANGE; }
     const bool has_ops = b.q_ops && b.t_ops;
+    // gasalx_packed_pairs reads the packed launch flags of this call only: a call that launches
+    // no packed kernel (or reuses misc for other flags, the KSW / banded / local16 todo arrays)
+    // must not leave the last call's count behind
+    ws.pk_flags = 0;
     BatchShape sized = shape;
     sized.n = b.n_alns;
     Plan pl = make_plan(p, sized, has_ops);
@@ -757,9 +762,9 @@ int align_device(Workspace &ws, const gasalx_params &p, const gasalx_batch &b, c
         }
     }
 
-    // (one launch pair: the walk is latency-bound -- a 25 K-pair chunk's walk takes 0.51 ms, the
-    // whole 100 K-pair batch's 0.70 ms, profiles/r03_tb_chunks.md -- so chunking only added DP
-    // tails; round 4's chunk and tail-split paths measured no gain and are gone)
+    // (one launch chain: the walk is latency-bound -- ~600 dependent steps whatever the batch size --
+    // so splitting a call into halves whose walks overlap the next half's DP leaves the last walk
+    // exposed and gained nothing; round 6 measured it, profiles/r06/)
     return align_body(ws, p, pl, b, out, st, sized, cigar_cap, walk_qseq);
 }
 

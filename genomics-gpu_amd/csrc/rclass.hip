@@ -16,23 +16,28 @@ namespace gx {
 
 // the block's longest padded register axis.  The reverse pass's slots are sorted longest first
 // by exactly these words (start.hpp rev_bucket: SEMI the reversed target's, LOCAL the reversed
-// query's first), so it is the block's first slot's: two scalar loads.  Without a sort, the
-// maximum over the block's slots.  (A pair longer than the chosen G*R declines its block to the
+// query's first), so it is the block's first slot's: two scalar loads (A.perm_xkey).  Otherwise
+// the maximum over the block's slots.  (A pair longer than the chosen G*R declines its block to the
 // int32 kernel: wf16_body.inc's `other`.)
 template <int ALGO_, int G>
 __device__ __forceinline__ uint32_t block_xpad(const WfArgs &A) {
     constexpr bool TR = ALGO_ == WF16_SEMI_STOP;   // SEMI: X = target
     constexpr uint32_t ppb = kWavesPerBlock * 2 * (64 / G);
     const uint32_t base = blockIdx.x * ppb;
-    if (A.perm) {
+    if (A.perm && A.perm_xkey) {
         const uint32_t p0 = A.perm[base];
         return ((TR ? A.tlen[p0] : A.qlen[p0]) + 7u) & ~7u;
     }
+    // unsorted, or sorted by another key (LOCAL's slot sort drops the query key when its
+    // two-key histogram would not fit LDS): the maximum over the block's slots
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t m = 0;
     for (uint32_t i = lane; i < ppb; i += 64) {
         const uint32_t idx = base + i;
-        if (idx < A.n) m = max(m, ((TR ? A.tlen[idx] : A.qlen[idx]) + 7u) & ~7u);
+        if (idx < A.n) {
+            const uint32_t pr = A.perm ? A.perm[idx] : idx;
+            m = max(m, ((TR ? A.tlen[pr] : A.qlen[pr]) + 7u) & ~7u);
+        }
     }
 #pragma unroll
     for (int s = 32; s >= 1; s >>= 1) m = max(m, (uint32_t)__shfl_xor(m, s));

@@ -73,6 +73,9 @@ struct WfArgs {
     // (per pair) are the reversed lengths L, position p of a reversed sequence is position L-1-p at
     // the pair's offset, positions p >= L are N (nval)
     int32_t rev;
+    // rclass.hip: the slots (perm) are sorted longest first by the register-axis words, so a
+    // block's first slot is its longest; 0: perm follows another key (block maximum taken)
+    int32_t perm_xkey;
 };
 
 constexpr int kWavesPerBlock = 4;

@@ -295,7 +295,10 @@ int gasalx_nv_banded_score_host(gasalx_engine *eng, const gasalx_nv_aligner *ali
  * before the pushes and clip(source.y) after them (nvbio_batched.h replays both).
  * ops_stride >= max pattern + max text length; nvbio's int16 DP columns bound
  * (max pattern + max text + 2) * max |score| <= 32767, and pattern x text <= 16 M cells.
- * Workspace: pad8(pattern) x text bytes + 8 bytes per text symbol per pair, held by the engine. */
+ * Workspace: pad8(pattern) x text bytes + 8 bytes per text symbol per pair, held by the engine; a
+ * batch runs in chunks of at most 4 GB of it (gasalx_nv_traceback_workspace gives the bytes a
+ * call reserves).  Calls that share an engine must be serialised (one workspace per engine). */
+uint64_t gasalx_nv_traceback_workspace(uint32_t max_pattern_len, uint32_t max_text_len, uint32_t n_pairs);
 int gasalx_nv_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t n_pairs,
                                const gasalx_nv_strings *dev_patterns, const gasalx_nv_strings *dev_texts,
                                uint32_t max_pattern_len, uint32_t max_text_len, int32_t *dev_scores,
@@ -313,7 +316,10 @@ int gasalx_nv_traceback_host(gasalx_engine *eng, const gasalx_nv_aligner *aligne
  * pushes in push order; INT32_MIN and (-1, -1) ends for a pair whose text is shorter than its
  * pattern.  ED, SW and Gotoh aligners.  ops_stride >= 2 x max pattern + band; nvbio's int16
  * checkpoints bound (max pattern + band + 3) * max |score| <= 32736.  Workspace: max pattern x
- * pad4(band) bytes per pair, held by the engine.  max_pattern_len 0 = read back. */
+ * pad4(band) bytes per pair, held by the engine, in chunks of at most 4 GB
+ * (gasalx_nv_banded_traceback_workspace); calls sharing an engine must be serialised.
+ * max_pattern_len 0 = read back. */
+uint64_t gasalx_nv_banded_traceback_workspace(uint32_t max_pattern_len, uint32_t band, uint32_t n_pairs);
 int gasalx_nv_banded_traceback_device(gasalx_engine *eng, const gasalx_nv_aligner *aligner, uint32_t band,
                                       uint32_t n_pairs, const gasalx_nv_strings *dev_patterns,
                                       const gasalx_nv_strings *dev_texts, uint32_t max_pattern_len,

@@ -287,9 +287,16 @@ struct BatchedAlignmentTraceback {
     typedef stream_type input_stream_type;
     typedef typename stream_type::aligner_type aligner_type;
 
-    // the workspace (flags of every cell, one DP row per pair) is the engine's, not the caller's
-    static uint64 min_temp_storage(const uint32, const uint32, const uint32) { return 0; }
-    static uint64 max_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+    // the workspace (flags of every cell, one DP row per pair) is the engine's, not the caller's:
+    // these report what enact() reserves in it (batches past 4 GB of it run in chunks), so a
+    // caller sizing its batches from them sees the device memory a call takes.
+    // enact() calls sharing one engine() must be serialised: they share that workspace.
+    static uint64 min_temp_storage(const uint32 max_pattern_len, const uint32 max_text_len, const uint32) {
+        return gasalx_nv_traceback_workspace(max_pattern_len, max_text_len, 1);
+    }
+    static uint64 max_temp_storage(const uint32 max_pattern_len, const uint32 max_text_len, const uint32 n) {
+        return gasalx_nv_traceback_workspace(max_pattern_len, max_text_len, n);
+    }
 
     void enact(stream_type stream, uint64 temp_size = 0u, uint8 *temp = NULL, void *hip_stream = NULL) {
         (void)temp_size; (void)temp;
@@ -318,8 +325,13 @@ struct BatchedBandedAlignmentTraceback {
     typedef stream_type input_stream_type;
     typedef typename stream_type::aligner_type aligner_type;
 
-    static uint64 min_temp_storage(const uint32, const uint32, const uint32) { return 0; }
-    static uint64 max_temp_storage(const uint32, const uint32, const uint32) { return 0; }
+    // the engine's workspace a call reserves (see BatchedAlignmentTraceback)
+    static uint64 min_temp_storage(const uint32 max_pattern_len, const uint32, const uint32) {
+        return gasalx_nv_banded_traceback_workspace(max_pattern_len, BAND_LEN, 1);
+    }
+    static uint64 max_temp_storage(const uint32 max_pattern_len, const uint32, const uint32 n) {
+        return gasalx_nv_banded_traceback_workspace(max_pattern_len, BAND_LEN, n);
+    }
 
     void enact(stream_type stream, uint64 temp_size = 0u, uint8 *temp = NULL, void *hip_stream = NULL) {
         (void)temp_size; (void)temp;

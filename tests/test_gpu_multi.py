@@ -263,16 +263,22 @@ def test_multi_pairhmm_device_resident_shards_and_gather():
     m.close()
 
 
-@pytest.mark.parametrize("workload,pairs,checked,world", [("semi", 200_000, 200_000, 2), ("nw_tb", 20_000, 40_000, 2),
-                                                          ("pairhmm", 8_000, 16_000, 2), ("semi", 200_000, 200_000, 4)])
-def test_bench_ranks_gloo_one_gpu(workload, pairs, checked, world):
+@pytest.mark.parametrize("workload,pairs,checked,world,warm", [("semi", 200_000, 200_000, 2, "1"),
+                                                               ("nw_tb", 20_000, 40_000, 2, "1"),
+                                                               ("pairhmm", 8_000, 16_000, 2, "1"),
+                                                               ("semi", 200_000, 200_000, 4, "1"),
+                                                               ("semi", 200_000, 200_000, 2, None)])
+def test_bench_ranks_gloo_one_gpu(workload, pairs, checked, world, warm):
     # the exact N-rank bench path on one device: torch.distributed.run spawns the ranks, each
     # aligns its cell-balanced shard into ScoreGather.buf, the gloo exchange runs in every
     # timed step, and rank 0 checks the gathered scores of every rank against the oracle.
     # nw_tb runs several engines on their own streams per rank (its default), each with its own
-    # exchange buffers; pairhmm gathers fp32 results (config 5, "1 -> 8 GPUs"); semi at world 4
+    # exchange buffers; pairhmm gathers fp32 results (config 5, "1 -> 8 GPUs"); semi at world 4.
+    # warm None: the default time-based warmup, whose stop decision the ranks take together
+    # (each rank's own clock could leave the ranks in different collectives)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
-           "--workload", workload, "--pairs", str(pairs), "--steps", "3", "--warmup", "1", "--no-e2e"]
+           "--workload", workload, "--pairs", str(pairs), "--steps", "3", "--no-e2e"]
+    cmd += ["--warmup", warm] if warm else ["--warmup-seconds", "0.3"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
