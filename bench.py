@@ -100,6 +100,12 @@ WORKLOADS = {
                 label="GASAL2 KSW (ksw_kernel_template.h:47-199, BWA ksw_extend semantics) on config-2 data, 1M "
                       "pairs x 150bp per GPU, seed score 10 per pair; cells = the full rectangle (the kernel "
                       "trims, as the reference does)"),
+    "boundary": dict(kind=7, pairs=1_000_000, scaling="weak", params=dict(algo=G.LOCAL), bytes=None, ops=12,
+                     label="the drop-in boundary driven as the reference's test_prog drives it (test_prog.cpp:12,18,"
+                           "202-347): T host threads x 2 gasal_gpu_storage x 5,000-pair host batches through "
+                           "gasal_host_batch_fill / gasal_aln_async / gasal_is_aln_async_done, SW local score + "
+                           "ends, over the reference's 20K sample pairs (query 150 bp, target 152-277 bp) "
+                           "replicated to 1M pairs; host pages to host results, PCIe included"),
     "cpu_plumbing": dict(kind=1, pairs=1024, scaling="weak", params=dict(algo=G.LOCAL), bytes=152, ops=12,
                          label="config1: 1024 pairs 64x64 SW local through the host-side CPU verify scorer "
                                "(oracle/), same batch through the GPU, seed 0x5EED0001"),
@@ -109,6 +115,7 @@ METRICS = {
     "nvbio_gotoh": "GCUPS of nvbio-style batched Gotoh semi-global scoring (sw-benchmark idiom) on MI355X",
     "nvbio_banded": "GCUPS (band cells) of nvbio-style banded (16) Gotoh semi-global scoring on MI355X",
     "cpu_plumbing": "GCUPS of the repo's host-side CPU verify scorer (config 1, 1024 x 64x64)",
+    "boundary": "GCUPS end to end through gasal_aln_async (test_prog pattern, host batches to host results) on MI355X",
     "ksw": "GCUPS of GASAL2 KSW extension (config-2 data, 1M x 150bp) on MI355X",
     "sw_local_300": "GCUPS of batched 300bp affine-gap SW local (config-3 data) on MI355X",
     "nw_score": "GCUPS of batched 300bp affine-gap NW global score (config-3 data) on MI355X",
@@ -150,6 +157,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo stages the exchange "
                          "through host memory, so several ranks can share one GPU)")
+    ap.add_argument("--threads", default="1,2,4,8",
+                    help="boundary workload: host thread counts to run (test_prog -n), comma separated")
+    ap.add_argument("--batch-pairs", type=int, default=5000,
+                    help="boundary workload: pairs per host batch (test_prog's STREAM_BATCH_SIZE = 5,000)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's shard of the global batch as a JSON line and exit (no GPU call)")
     return ap.parse_args()
@@ -578,6 +589,128 @@ def run_cpu_plumbing(args, wl):
     print(json.dumps(out), flush=True)
 
 
+# --------------------------------------------------------------- boundary -
+def run_boundary(args, wl):
+    """The drop-in boundary the way the reference's test_prog uses it (tools/boundary_bench.cpp: T
+    OpenMP threads x 2 storages x 5,000-pair batches through gasal_host_batch_fill / gasal_aln_async
+    / gasal_is_aln_async_done), over the reference's own 20K sample pairs replicated to --pairs;
+    every pair of the last pass checked against the oracle; beside it the flat host entry point
+    (gasalx_align_host) and the device-resident call (gasalx_align_device) on the same pairs."""
+    import gzip
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import read_fasta_pairs
+    exe = os.path.join(ROOT, "tools", "boundary_bench")
+    if not os.path.exists(exe):
+        sys.exit("bench.py: tools/boundary_bench is not built (make -C tools)")
+    tmp = tempfile.mkdtemp(prefix="gasal_boundary_")
+    paths = []
+    for name in ("query_batch.fasta.gz", "target_batch.fasta.gz"):
+        dst = os.path.join(tmp, name[:-3])
+        with gzip.open(os.path.join(ROOT, "tests", "golden", name), "rb") as fi, open(dst, "wb") as fo:
+            fo.write(fi.read())
+        paths.append(dst)
+    q, t, _, _ = read_fasta_pairs()
+    base = len(q)
+    repl = max(1, (args.pairs or wl["pairs"]) // base)
+    n = base * repl
+    cells = int(sum(len(a) * len(b) for a, b in zip(q, t))) * repl
+    runs, dumps = [], {}
+    for T in [int(x) for x in args.threads.split(",") if x]:
+        dump = os.path.join(tmp, f"res_{T}.bin")
+        cmd = [exe, "--repl", str(repl), "--batch", str(args.batch_pairs),
+               "--warm", str(1 if args.warmup is None else max(1, args.warmup)),
+               "--reps", str(max(1, min(args.steps, 5))), "--dump", dump, "-y", "local", "-n", str(T)] + paths
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            sys.exit(f"bench.py: boundary_bench -n {T} failed: {r.stderr[-2000:]}")
+        line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        runs.append(line)
+        dumps[T] = dump
+    best = max(runs, key=lambda x: x["gcups"])
+    # parity: the oracle over the 20K sample pairs, every replica of every run against it
+    O = _oracle(native=not args.no_cpu)
+    batch = G.Batch.from_pairs(q, t)
+    t_o = time.perf_counter()
+    ref = oracle_align(O, batch, wl["params"], oracle_threads())
+    oracle_s = time.perf_counter() - t_o
+    mism = {}
+    for T, path in dumps.items():
+        got = np.fromfile(path, np.int32).reshape(5, n)
+        bad = 0
+        for k, f in enumerate(("score", "q_end", "t_end")):
+            bad += int(np.count_nonzero(got[k].reshape(repl, base) != ref[f][None, :]))
+        mism[f"threads_{T}"] = bad
+    # the flat host entry point and the device-resident call on the same (tiled) pairs
+    big = G.Batch(np.tile(batch.q_data, repl),
+                  (batch.q_offsets[None, :].astype(np.int64) + np.arange(repl)[:, None] * batch.q_bytes)
+                  .reshape(-1).astype(np.uint32), np.tile(batch.q_lens, repl),
+                  np.tile(batch.t_data, repl),
+                  (batch.t_offsets[None, :].astype(np.int64) + np.arange(repl)[:, None] * batch.t_bytes)
+                  .reshape(-1).astype(np.uint32), np.tile(batch.t_lens, repl))
+    params = G.make_params(**wl["params"])
+    eng = G.Engine(0)
+    fields = ["score", "q_end", "t_end"]
+    eng.align_host(big, params, fields=fields)
+    th = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        gh = eng.align_host(big, params, fields=fields)
+        th.append(time.perf_counter() - t0)
+    host_bad = sum(int(np.count_nonzero(gh[f].reshape(repl, base) != ref[f][None, :])) for f in fields)
+    dev = torch.device("cuda", 0)
+    as_i32 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    d = {"q_batch": torch.from_numpy(big.q_data).to(dev), "t_batch": torch.from_numpy(big.t_data).to(dev),
+         "q_offsets": as_i32(big.q_offsets), "t_offsets": as_i32(big.t_offsets), "q_lens": as_i32(big.q_lens),
+         "t_lens": as_i32(big.t_lens), "aln_score": torch.empty(n, dtype=torch.int32, device=dev),
+         "q_end": torch.empty(n, dtype=torch.int32, device=dev), "t_end": torch.empty(n, dtype=torch.int32, device=dev)}
+    ptrs = {k: v.data_ptr() for k, v in d.items()}
+    stream = torch.cuda.Stream(dev)
+    mq, mt = int(big.q_lens.max()), int(big.t_lens.max())
+    for _ in range(3):
+        eng.align_device_ptrs(params, ptrs, big.q_bytes, big.t_bytes, n, mq, mt, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a, b in evs:
+        a.record(stream)
+        eng.align_device_ptrs(params, ptrs, big.q_bytes, big.t_bytes, n, mq, mt, stream.cuda_stream)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    dev_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    dev_bad = sum(int(np.count_nonzero(d[k].cpu().numpy().reshape(repl, base) != ref[f][None, :]))
+                  for k, f in (("aln_score", "score"), ("q_end", "q_end"), ("t_end", "t_end")))
+    plan = G.describe_plan(params, mq, mt)
+    eng.close()
+    out = {"metric": METRICS["boundary"], "value": best["gcups"], "unit": "GCUPS", "n_gpus": 1,
+           "steps": len(best["pass_ms"]), "warmup": 1 if args.warmup is None else max(1, args.warmup),
+           "ms_per_step": best["best_ms"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": dtype_label(plan, 2),
+           "data": "the reference's test_prog sample pairs (tests/golden/*_batch.fasta.gz), replicated",
+           "config": {"workload": wl["label"], "pairs": n, "base_pairs": base, "replicas": repl, "cells": cells,
+                      "threads_best": best["threads"], "storages_per_thread": best["storages"],
+                      "batch_pairs": best["batch"], "plan_of_a_batch": G.describe_plan(params, mq, mt)},
+           "runs": runs,
+           "vs_reference_a100_derived": {"end_to_end_48.6": round(best["gcups"] / 48.6, 2),
+                                         "kernel_window_80": round(best["gcups"] / 80.0, 2),
+                                         "source": "BASELINE.md section 1 (CDP/GASAL2/test_prog/report1.sqlite)"},
+           "flat_host_entry": {"value": round(cells / min(th) / 1e9, 2), "ms": round(min(th) * 1e3, 3),
+                               "mismatches": host_bad,
+                               "path": "gasalx_align_host on the same pairs (pageable arrays; chunks on two streams)"},
+           "device_resident": {"value": round(cells / dev_ms / 1e6, 2), "ms": round(dev_ms, 3), "mismatches": dev_bad,
+                               "plan": plan,
+                               "path": "gasalx_align_device on the same pairs in HBM (HIP events around the call)"},
+           "parity": {"pairs_checked": n * len(dumps), "mismatches": sum(mism.values()), "by_run": mism,
+                      "tolerance": "bit-exact", "against": "oracle/ over the 20K sample pairs; every replica of "
+                                                          "every run's last pass compared with it"}}
+    if not args.no_cpu:
+        out["cpu_baseline"] = {"value": round(cells / repl / oracle_s / 1e9, 4), "unit": "GCUPS",
+                               "cores": oracle_threads(), "kind": "port",
+                               "sample": f"the {base} sample pairs once (the parity run, {oracle_s:.2f} s)"}
+    print(json.dumps(out), flush=True)
+    if out["parity"]["mismatches"] or host_bad or dev_bad:
+        sys.exit(3)
+
+
 # ------------------------------------------------------------------ main ----
 def main():
     args = parse()
@@ -592,6 +725,10 @@ def main():
         if world != 1:
             sys.exit("bench.py: cpu_plumbing is a 1-process workload")
         return run_cpu_plumbing(args, wl)
+    if args.workload == "boundary":
+        if world != 1:
+            sys.exit("bench.py: the boundary workload runs one process (its host threads share the GPU)")
+        return run_boundary(args, wl)
 
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

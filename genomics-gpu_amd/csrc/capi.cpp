@@ -888,7 +888,10 @@ extern "C" int gasalx_packed_pairs(gasalx_engine *e, uint64_t *handled, uint64_t
         std::vector<uint8_t> f(ws.pk_flags);
         CK(hipMemcpy(f.data(), ws.misc.p, f.size(), hipMemcpyDeviceToHost));
         for (uint32_t i = 0; i < ws.pk_flags; i++) {
-            const uint64_t lo = (uint64_t)i * ws.pk_ppb, hi = std::min<uint64_t>(lo + ws.pk_ppb, ws.pk_pairs);
+            // (a mixed-shape launch: the blocks from pk_b1 on cover pk_ppb2 pairs from pk_p1 on)
+            const bool t2 = ws.pk_p1 != 0xFFFFFFFFu && i >= ws.pk_b1;
+            const uint64_t lo = t2 ? (uint64_t)ws.pk_p1 + (uint64_t)(i - ws.pk_b1) * ws.pk_ppb2 : (uint64_t)i * ws.pk_ppb;
+            const uint64_t hi = std::min<uint64_t>(lo + (t2 ? ws.pk_ppb2 : ws.pk_ppb), ws.pk_pairs);
             if (hi > lo && f[i]) *handled += hi - lo;
         }
         *total += ws.pk_pairs;

@@ -263,6 +263,7 @@ static bool local16_ok(const gasalx_params &p, uint32_t q8, uint32_t t8) {
 
 Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
     Plan pl;
+    pl.max_q = s.max_q; pl.max_t = s.max_t;
     const uint32_t q8 = pad8(s.max_q), t8 = pad8(s.max_t);
     const bool tb = p.start_pos == 2;
     int wf_algo = -1;
@@ -469,6 +470,72 @@ static hipError_t copy_d2d(void *dst, const void *src, size_t bytes, hipStream_t
     return e;
 }
 
+// The short second shape of a packed score launch (wf16_mix_kernel): more lanes per pair and
+// fewer rows per lane, a wave a third as long, over the launch's last slots.  Taken for the
+// score plans it is instantiated for (LOCAL in the e-drift frame with f16 keys at G8R19, 150 bp:
+// config 2; GLOBAL score at G16R20, 300 bp), when the launch holds at least two rounds of its
+// waves and the value window and key range also hold for the second shape's span.  The slots
+// past the last whole round of long waves (GASALX_TAIL_K more rounds: 0 by default) take it;
+// GASALX_TAIL=0: one shape (A/B).
+struct TailShape {
+    WfFn fn = nullptr;
+    uint32_t b0 = 0, p0 = 0, ppb = 1, lds_stride = 0;
+    size_t lds_bytes = 0;
+    int32_t vmin = 0;   // GLOBAL: the value-window bound for the larger span of the two shapes
+};
+static TailShape tail_shape(const Plan &pl, const gasalx_params &p, const WfArgs &A, uint32_t n) {
+    TailShape t;
+    // (read per call, so a test process can compare both)
+    const bool on = env_flag("GASALX_TAIL", true);
+    const char *ke = std::getenv("GASALX_TAIL_K");
+    const int kextra = ke ? std::atoi(ke) : 0;
+    if (!on || !pl.packed16 || pl.tb || pl.key2 || pl.ku16 || pl.kseg_shift || pl.semi_tq || A.rev || A.n_dev ||
+        A.stop || A.lstop)
+        return t;
+    int G2 = 0, R2 = 0;
+    WfFn fn = nullptr;
+    if (pl.wf_algo == WF_LOCAL && pl.kf16 && pl.G16 == 8 && pl.R16 == 19) {
+        G2 = 32; R2 = 5; fn = &wf16_mix_kernel<WF_LOCAL, 8, 19, 32, 5>;
+    } else if (pl.wf_algo == WF_GLOBAL && pl.G16 == 16 && pl.R16 == 20) {
+        G2 = 64; R2 = 5; fn = &wf16_mix_kernel<WF_GLOBAL, 16, 20, 64, 5>;
+    } else {
+        return t;
+    }
+    const int64_t q8 = pad8(pl.max_q), y8 = pad8(pl.max_t);   // LOCAL / GLOBAL: the target is the step axis
+    // the second shape's span and keys must fit the value window too (make_plan checked the first's)
+    const int64_t span2 = (int64_t)G2 * R2 + y8 + 2 * G2 + 8;
+    if (pl.wf_algo == WF_LOCAL) {
+        const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
+        const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
+        const int64_t hmax = a * std::min(q8, y8), base = 0x400 + oe + k + 16;
+        if (!(base + hmax + e * span2 + a + k + 64 <= 0x7BFF && (hmax + 1) * (y8 + G2) <= 0x7800)) return t;
+        t.vmin = pl.vmin;
+    } else {
+        // the window offset for the larger span serves both shapes: their values then sit higher
+        // in the same window, whose top packed16_ok checked for that span
+        if (!packed16_ok(p, WF_GLOBAL, pl.max_q, pl.max_t, &t.vmin, std::max<int64_t>(span2, (int64_t)pl.G16 * pl.R16 + y8 + 2 * pl.G16 + 8)))
+            return t;
+        t.vmin = std::max(t.vmin, pl.vmin);
+    }
+    static int cus = 0;
+    if (!cus) { int d = 0; (void)hipGetDevice(&d); (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d); }
+    const uint64_t slots = (uint64_t)wf16_waves(pl.wf_algo, pl.R16) * 4 * (cus > 0 ? cus : 256);
+    const uint32_t ppw = 2 * (64 / pl.G16), ppb = kWavesPerBlock * ppw;
+    const uint64_t waves = (n + ppw - 1) / ppw;
+    const uint64_t rounds = waves / slots;
+    if (rounds < 2 + (uint64_t)std::max(kextra, 0)) return t;
+    const uint64_t long_waves = (rounds - (uint64_t)std::max(kextra, 0)) * slots;
+    t.b0 = (uint32_t)(long_waves / kWavesPerBlock);
+    t.p0 = t.b0 * ppb;
+    if (t.p0 >= n) return TailShape();
+    t.ppb = kWavesPerBlock * 2 * (64 / G2);
+    const uint32_t words = ((uint32_t)y8 + 2 * G2 + 4 + 3) & ~3u;   // as make_plan's, for G2
+    t.lds_stride = words * 8;
+    t.lds_bytes = (size_t)kWavesPerBlock * (64 / G2) * t.lds_stride;
+    t.fn = fn;
+    return t;
+}
+
 // Launch the wavefront kernel(s) of plan `pl` over one device batch: the packed
 // kernel first when the plan has one (it flags the blocks it aligned), then the
 // int32 kernel, which aligns exactly the pairs of the declined blocks.
@@ -491,10 +558,21 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         P16.vmin = pl.vmin;
         P16.kf16 = pl.kf16;
         const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
-        const uint32_t grid16 = grid_for(n, ppb16);
+        uint32_t grid16 = grid_for(n, ppb16);
+        // the launch's last slots on a shorter shape (wavefront16.hpp wf16_mix_kernel), so that its
+        // end is not a fraction of a round of long waves running alone
+        const TailShape tail = tail_shape(pl, p, A, n);
+        size_t lds16 = pl.lds16_bytes;
+        if (tail.fn) {
+            P16.tail_b0 = tail.b0; P16.tail_p0 = tail.p0; P16.tail_lds = tail.lds_stride;
+            P16.vmin = tail.vmin;
+            grid16 = tail.b0 + grid_for(n - tail.p0, tail.ppb);
+            lds16 = std::max(lds16, tail.lds_bytes);
+        }
         HIPCHK(ws.misc.reserve(grid16 + 64));
         P16.handled = ws.misc.as<uint8_t>();
         ws.pk_flags = grid16; ws.pk_ppb = ppb16; ws.pk_pairs = n;
+        ws.pk_p1 = tail.fn ? tail.p0 : 0xFFFFFFFFu; ws.pk_b1 = tail.b0; ws.pk_ppb2 = tail.fn ? tail.ppb : 1;
         if (pl.tb) {
             HIPCHK(ws.aux.reserve((size_t)n * 4));
             P16.tbfix = ws.aux.as<int32_t>();
@@ -519,15 +597,18 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
             P16.kseg_shift = pl.kseg_shift;
             P16.kseg_n = nsave;
         }
+        if (tail.fn) f16 = tail.fn;
         if (!f16) { set_error("no packed wavefront instance"); return GASALX_EUNSUPPORTED; }
-        if (pl.lds16_bytes > 64 * 1024)
-            HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)pl.lds16_bytes));
-        hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), pl.lds16_bytes, st, P16);
+        if (lds16 > 64 * 1024)
+            HIPCHK(hipFuncSetAttribute((const void *)f16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds16));
+        hipLaunchKernelGGL(f16, dim3(grid16), dim3(kBlock), lds16, st, P16);
         HIPCHK(hipGetLastError());
         // ... and the int32 kernel aligns the pairs of the blocks it declined
         A.skip = ws.misc.as<uint8_t>();
         A.skip_ppb = ppb16;
+        A.skip_p1 = tail.fn ? tail.p0 : 0xFFFFFFFFu;
+        A.skip_b1 = tail.b0;
+        A.skip_ppb2 = tail.fn ? tail.ppb : 1;
     }
     WfFn fn = A.stop ? wf_pick_stop(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
@@ -603,6 +684,7 @@ static int launch_semi_tq(Workspace &ws, const Plan &pl, const gasalx_params &p,
     }
     A.skip = ws.misc.as<uint8_t>();
     A.skip_ppb = 1;
+    A.skip_p1 = 0xFFFFFFFFu;
     WfFn fn = wf_lookup(pl.wf_algo, pl.keys, false, pl.G, pl.R);
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
     if (pl.lds_bytes > 64 * 1024)

@@ -40,6 +40,9 @@ struct Workspace {
     // the last packed launch's "aligned here" flags in misc (gasalx_packed_pairs): flag count, pairs
     // per flag, pairs of the launch (0 flags: no packed launch yet)
     uint32_t pk_flags = 0, pk_ppb = 0, pk_pairs = 0;
+    // a mixed-shape launch (wavefront16.hpp wf16_mix_kernel): flags from pk_b1 on cover pk_ppb2 pairs
+    // each, from pair pk_p1 on (pk_p1 = 0xFFFFFFFF: one block size)
+    uint32_t pk_p1 = 0xFFFFFFFFu, pk_b1 = 0, pk_ppb2 = 1;
     void release_all();
 };
 
@@ -68,6 +71,7 @@ struct Plan {
     bool semi_tq = false;   // SEMI TAIL=QUERY/BOTH: packed class launches (one per padded target length), int32 fallback
     bool tb_band = false;   // packed GLOBAL+TB by band recomputation (wavefront16.hpp WF16_GLOBAL_CP / _BAND)
     uint32_t band_w = 0, band_wd = 0;
+    uint32_t max_q = 0, max_t = 0;   // the batch shape the plan was made for
     std::string name;
 };
 

@@ -54,6 +54,7 @@ __device__ __forceinline__ uint32_t block_xpad(const WfArgs &A) {
 template <int ALGO_, int G, int R0, int R1, int R2, int R3, int R4, int R5>
 __global__ __launch_bounds__(kBlock, wf16_waves(ALGO_, R5 ? R5 : R4 ? R4 : R3)) void wf16_rclass_kernel(WfArgs A) {
     const uint32_t need = block_xpad<ALGO_, G>(A);
+    const uint32_t wf16_bid = blockIdx.x, wf16_bl = blockIdx.x, wf16_p0 = 0, wf16_lds = A.lds_stride;
     if (need <= (uint32_t)(G * R0)) {
         constexpr int R = R0;
 #include "wf16_body.inc"
@@ -79,6 +80,7 @@ __global__ __launch_bounds__(kBlock, wf16_waves(ALGO_, R5 ? R5 : R4 ? R4 : R3)) 
 
 template <int ALGO_, int G, int R>
 __device__ __attribute__((always_inline)) void wf16_body(const WfArgs &A) {
+    const uint32_t wf16_bid = blockIdx.x, wf16_bl = blockIdx.x, wf16_p0 = 0, wf16_lds = A.lds_stride;
 #include "wf16_body.inc"
 }
 

@@ -76,7 +76,17 @@ struct WfArgs {
     // rclass.hip: the slots (perm) are sorted longest first by the register-axis words, so a
     // block's first slot is its longest; 0: perm follows another key (block maximum taken)
     int32_t perm_xkey;
+    // wavefront16.hpp wf16_mix_kernel: the short shape's first block and slot, its LDS bytes per slot
+    uint32_t tail_b0, tail_p0, tail_lds;
+    // int32 kernel after a mixed launch: slots from skip_p1 on have their flags from skip_b1 on, one
+    // per skip_ppb2 slots (skip_p1 = 0xFFFFFFFF: one flag per skip_ppb slots throughout)
+    uint32_t skip_p1, skip_b1, skip_ppb2;
 };
+
+// the packed launch's flag covering slot idx (wf16_mix_kernel: two block sizes)
+__device__ __forceinline__ uint32_t skip_flag(const WfArgs &A, uint32_t idx) {
+    return idx < A.skip_p1 ? idx / A.skip_ppb : A.skip_b1 + (idx - A.skip_p1) / A.skip_ppb2;
+}
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
@@ -406,7 +416,7 @@ __device__ __forceinline__ void wf_block(const WfArgs &A, uint8_t *lds, const ui
     const uint32_t idx = pair0 + slot;   // slot; the pair is perm[slot] when sorted
     // pairs the packed kernel already aligned are skipped (dispatch.hip); its flags are per block of slots
     const uint32_t nn = A.n_dev ? min(*A.n_dev, A.n) : A.n;   // (traceback fallback: a device-side count)
-    const bool valid = idx < nn && !(A.skip && A.skip[idx / A.skip_ppb]);
+    const bool valid = idx < nn && !(A.skip && A.skip[skip_flag(A, idx)]);
     const uint32_t pair = (valid && A.perm) ? A.perm[idx] : idx;
     if (A.skip && !__syncthreads_or(valid)) return;      // block-uniform early exit
 
@@ -484,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void wf_kernel(WfArgs A) {
         const uint32_t bx = base + lane * gridDim.x;
         bool run = bx < nblk;
         if (run && A.skip) {   // a declined pair: some flag over its slots is clear
-            const uint32_t f0 = bx * PPB / A.skip_ppb, f1 = (min(bx * PPB + PPB, A.n) - 1) / A.skip_ppb;
+            const uint32_t f0 = skip_flag(A, bx * PPB), f1 = skip_flag(A, min(bx * PPB + PPB, A.n) - 1);
             bool all = true;
             for (uint32_t f = f0; f <= f1; ++f) all &= A.skip[f] != 0;
             run = !all;

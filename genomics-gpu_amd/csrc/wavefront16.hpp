@@ -553,7 +553,29 @@ __host__ __device__ constexpr int wf16_waves(int algo, int R) {
 
 template <int ALGO_, int G, int R>
 __global__ __launch_bounds__(kBlock, wf16_waves(ALGO_, R)) void wf16_kernel(WfArgs A) {
+    const uint32_t wf16_bid = blockIdx.x, wf16_bl = blockIdx.x, wf16_p0 = 0, wf16_lds = A.lds_stride;
 #include "wf16_body.inc"
+}
+
+// One launch, two shapes: blocks [0, A.tail_b0) run (G1, R1) over slots [0, A.tail_p0), the rest run
+// (G2, R2) -- more lanes per pair, fewer rows per lane, so a wave is a third as long -- over the
+// slots from A.tail_p0 on.  Blocks are dispatched in order, so the short waves fill the slots the
+// long ones leave at the end of the launch instead of the last long waves running alone (a launch
+// of W waves over S resident slots ends with about one wave time at a fraction of the chip:
+// config 2 ran 1.7 % faster at 983,040 pairs, 20 full rounds, than at 1 M, profiles/r06/tail/).
+// The flags in A.handled follow the blocks (A.skip_* tell the int32 kernel their slot ranges).
+template <int ALGO_, int G1, int R1, int G2, int R2>
+__global__ __launch_bounds__(kBlock, wf16_waves(ALGO_, R1)) void wf16_mix_kernel(WfArgs A) {
+    if (blockIdx.x < A.tail_b0) {
+        constexpr int G = G1, R = R1;
+        const uint32_t wf16_bid = blockIdx.x, wf16_bl = blockIdx.x, wf16_p0 = 0, wf16_lds = A.lds_stride;
+#include "wf16_body.inc"
+    } else {
+        constexpr int G = G2, R = R2;
+        const uint32_t wf16_bid = blockIdx.x, wf16_bl = blockIdx.x - A.tail_b0, wf16_p0 = A.tail_p0,
+                       wf16_lds = A.tail_lds;
+#include "wf16_body.inc"
+    }
 }
 
 // SEMI TAIL=QUERY/BOTH instances, G = 8, R = 1..32 (semi_tq.hip; one per padded target

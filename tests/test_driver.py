@@ -122,3 +122,33 @@ def test_driver_output_contract(tmp_path, case):
         got = [g for g in got if g.split("\t")[0][len("query_name="):] not in names]
     # batches of different storages/threads may interleave; within a batch order is kept
     assert sorted(got) == sorted(want)
+
+
+BOUNDARY = os.path.join(ROOT, "tools", "boundary_bench")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,batch,repl", [(1, 5000, 1), (3, 5000, 2), (2, 1777, 1)])
+def test_boundary_bench_results(tmp_path, threads, batch, repl):
+    # tools/boundary_bench (bench.py --workload boundary): the reference's test_prog loop over the
+    # 20K sample pairs (gzip FASTA read directly), replicated; its dump of the last pass's results
+    # must equal the oracle on every replica of every pair, for any thread count and batch size
+    O.build()
+    assert os.path.exists(BOUNDARY), "tools/boundary_bench not built (__graft_entry__.build())"
+    g = os.path.join(ROOT, "tests", "golden")
+    dump = tmp_path / "res.bin"
+    cmd = [BOUNDARY, "--repl", str(repl), "--warm", "1", "--reps", "1", "--batch", str(batch), "--dump", str(dump),
+           "-y", "local", "-n", str(threads), os.path.join(g, "query_batch.fasta.gz"),
+           os.path.join(g, "target_batch.fasta.gz")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    import json
+    info = json.loads(line)
+    q, t, _, _ = helpers.read_fasta_pairs()
+    n = len(q)
+    assert info["pairs"] == n * repl and info["threads"] == threads and info["gcups"] > 0
+    o = O.align(G.Batch.from_pairs(q, t), O.make_params(algo=O.LOCAL))
+    got = np.fromfile(dump, np.int32).reshape(5, n * repl)
+    for k, f in enumerate(("score", "q_end", "t_end")):
+        assert np.array_equal(got[k].reshape(repl, n), np.broadcast_to(o[f], (repl, n))), f

@@ -1290,3 +1290,64 @@ def test_ksw16_equals_levels(engine, monkeypatch, kw):
     o = O.align(b, O.make_params(algo=G.KSW, **kw), seed_scores=seed)
     for f in ("score", "q_end", "t_end"):
         assert np.array_equal(r16[f], o[f]), f
+
+
+# ------------------------------------------------ mixed-shape (tail) launches ----
+def _device_align(engine, b, algo):
+    """One gasalx_align_device call over the whole batch in HBM (one packed launch: the host
+    pipeline would split it into chunks), through torch device buffers."""
+    import torch
+    dev = torch.device("cuda", 0)
+    u = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32) if a.dtype == np.uint32 else a).to(dev)
+    d = {"q_batch": u(b.q_data), "t_batch": u(b.t_data), "q_offsets": u(b.q_offsets), "t_offsets": u(b.t_offsets),
+         "q_lens": u(b.q_lens), "t_lens": u(b.t_lens)}
+    for f in ("aln_score", "q_end", "t_end"):
+        d[f] = torch.full((b.n,), -7, dtype=torch.int32, device=dev)
+    engine.align_device_ptrs(G.make_params(algo=algo), {k: v.data_ptr() for k, v in d.items()}, b.q_bytes,
+                             b.t_bytes, b.n, int(b.q_lens.max()), int(b.t_lens.max()))
+    torch.cuda.synchronize()
+    return {"score": d["aln_score"].cpu().numpy(), "q_end": d["q_end"].cpu().numpy(),
+            "t_end": d["t_end"].cpu().numpy()}
+
+
+@pytest.mark.parametrize("kind,n,algo", [(2, 120_000, G.LOCAL), (3, 60_000, G.GLOBAL)])
+def test_tail_shape_launch(engine, monkeypatch, kind, n, algo):
+    """A launch of two or more rounds of packed waves runs its last slots on a shorter shape
+    (wavefront16.hpp wf16_mix_kernel; LOCAL G8R19 + G32R5 for config 2, GLOBAL G16R20 + G64R5 for
+    300 bp).  Results equal the oracle and the one-shape launch's, and the packed launch takes
+    every pair (its two flag ranges counted by gasalx_packed_pairs)."""
+    b = G.Batch.synth(kind, n, 0x7A11 + kind)
+    o = O.align(b, O.make_params(algo=algo))
+    fields = ("score",) if algo == G.GLOBAL else ("score", "q_end", "t_end")
+    monkeypatch.setenv("GASALX_TAIL", "1")
+    engine.packed_pairs()                                    # forget earlier launches
+    g = _device_align(engine, b, algo)
+    handled, total = engine.packed_pairs()
+    assert handled == total == n
+    monkeypatch.setenv("GASALX_TAIL", "0")
+    g0 = _device_align(engine, b, algo)
+    for f in fields:
+        assert np.array_equal(g[f], o[f]), f
+        assert np.array_equal(g0[f], o[f]), f
+
+
+@pytest.mark.parametrize("k_extra", ["0", "1"])
+def test_tail_shape_declined_blocks(engine, monkeypatch, k_extra):
+    """IUPAC codes in pairs of both shapes' ranges: their blocks decline to the int32 kernel, which
+    reads the mixed launch's two flag ranges (wavefront.hpp skip_flag); every pair exact."""
+    n = 120_000
+    b = G.Batch.synth(2, n, 0x7A20)
+    q = b.q_data.copy()
+    picks = [5, 70_000, n - 30_000, n - 5_000, n - 1_000, n - 17, n - 1]
+    for i in picks:
+        q[int(b.q_offsets[i]) + 3] = ord("R")
+    b = G.Batch(q, b.q_offsets, b.q_lens, b.t_data, b.t_offsets, b.t_lens)
+    o = O.align(b, O.make_params(algo=O.LOCAL))
+    monkeypatch.setenv("GASALX_TAIL", "1")
+    monkeypatch.setenv("GASALX_TAIL_K", k_extra)
+    engine.packed_pairs()
+    g = _device_align(engine, b, G.LOCAL)
+    handled, total = engine.packed_pairs()
+    assert total == n and n - 64 * len(picks) <= handled < n
+    for f in ("score", "q_end", "t_end"):
+        assert np.array_equal(g[f], o[f]), f
