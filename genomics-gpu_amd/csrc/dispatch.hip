@@ -116,7 +116,9 @@ static WfFn wf16_pick_local_tb(int G, int R) {   // R % 4 == 0 shapes
 
 static WfFn wf16_lookup(int algo, bool tb, int G, int R, bool key2 = false, bool stop = false, bool ku16 = false,
                         bool lrs = false, bool kseg = false, bool tbd = false) {
-    if (algo == WF_LOCAL) return tb ? (tbd ? wf16_pick_r4<WF16_LOCAL_TBD>(G, R) : wf16_pick_local_tb(G, R))
+    if (algo == WF_LOCAL) return tb ? (tbd ? (G == 16 && R == 12 ? &wf16_kernel<WF16_LOCAL_TBD, 16, 12>
+                                                                  : wf16_pick_r4<WF16_LOCAL_TBD>(G, R))
+                                           : wf16_pick_local_tb(G, R))
                                     : key2 ? wf16_pick<WF16_LOCAL_K2>(G, R)
                                                                : (ku16 || lrs || kseg) ? wf16_local_lookup(G, R, ku16, lrs, kseg)
                                                                                : wf16_pick<WF_LOCAL>(G, R);
@@ -322,10 +324,13 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
             if (gforce > 0) gmin = (uint32_t)gforce;
             // traceback kernels store flags in groups of 4 rows and keep >= 16 rows per
             // lane (their instances, wf16_pick_tb): the other shapes are never taken,
-            // forced or not
+            // forced or not -- except LOCAL+TB's G16R12 (3 waves per SIMD),
+            // taken under GASALX_LTBD_G16=1 for the A/B against the 2-wave G8R20
+            const bool ltbd16 = pl.tb && wf_algo == WF_LOCAL && env_flag("GASALX_LTBD_G16", false);
+            if (ltbd16) gmin = std::max<uint32_t>(gmin, 16);
             for (const Shape &sh : kShapes16)
                 if ((uint32_t)sh.G >= gmin && (uint32_t)(sh.G * sh.R) >= x8 &&
-                    !(pl.tb && (sh.R % 4 || (sh.G > 8 && sh.R < 16)))) {
+                    !(pl.tb && (sh.R % 4 || (sh.G > 8 && sh.R < 16)) && !(ltbd16 && sh.G == 16 && sh.R == 12))) {
                     pl.G16 = sh.G; pl.R16 = sh.R;
                     break;
                 }
@@ -380,6 +385,8 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 }
                 if (pl.kf16) pl.key2 = false;
             }
+            // (LOCAL+TB's G16R12, GASALX_LTBD_G16: an e-drift instance only)
+            if (wf_algo == WF_LOCAL && pl.tb && pl.G16 == 16 && pl.R16 == 12 && !pl.kf16) pl.packed16 = false;
             // outside both frames the round-2 keys must hold (packed16_ok admitted the drift case)
             if (wf_algo == WF_LOCAL && !pl.kf16 && !local_key16_ok(p, s.max_q, s.max_t)) pl.packed16 = false;
             pl.semi_tq = pl.semi_tq && pl.packed16;
@@ -929,7 +936,11 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         // uneven lengths: a wave's step count is set by its longest step-axis
         // sequence (target; query for the transposed SEMI kernel), so run the
         // slots in length order (counting sort, longest first)
-        if (sort_wanted(shape) && n >= 4096 && !pl.semi_tq) {   // (semi_tq sorts by target class itself)
+        // (semi_tq sorts by target class itself; a launch whose waves hold fewer than 8 pairs --
+        // the small-batch shapes, G >= 32 -- gains nothing from the order and would pay the three
+        // sort launches: a 5,000-pair batch of the reference's sample data, profiles/r06/boundary)
+        const int gsort = pl.packed16 ? pl.G16 : pl.G;
+        if (sort_wanted(shape) && n >= 4096 && !pl.semi_tq && 2 * (64 / std::max(gsort, 1)) >= 8) {
             const uint32_t s8w = pad8(pl.wf_algo == WF_SEMI ? shape.max_q : shape.max_t) / 8;
             const uint32_t *slen = pl.wf_algo == WF_SEMI ? b.q_lens : b.t_lens;
             const size_t sh = (size_t)(s8w + 1) * 4;

@@ -535,6 +535,7 @@ constexpr int WF16_LOCAL_U16_RS = 12; // the same with u16 keys (local_rs.hip in
 // row the first segment holding its maximum (later columns win only when strictly higher)
 constexpr int WF16_LOCAL_SEG = 13;
 constexpr int WF16_LOCAL_TBD = 14;    // LOCAL + traceback in the e-drift frame (step_local_tb_dr)
+constexpr int WF16_LOCAL_SEGR = 15;   // WF16_LOCAL_SEG with the finished segments' best per row in registers
 constexpr int kW16_LTBD_WAVES = 2;
 constexpr int kW16_TQ_WAVES = 3;
 constexpr int kW16_TQ_BIG_WAVES = 3;   // R > 20: 3 waves spill (R = 23: 20 VGPRs) and still beat 2 (profiles/r03_semi_tq_waves_ab.md)
@@ -544,7 +545,8 @@ constexpr int kW16_CP_WAVES = 3;    // GLOBAL score sweep with band checkpoints,
 __host__ __device__ constexpr int wf16_waves(int algo, int R) {
     return algo == WF16_GLOBAL_TB ? kW16_TB_WAVES
            : algo == WF16_LOCAL_TB ? kW16_LTB_WAVES
-           : algo == WF16_LOCAL_TBD ? kW16_LTBD_WAVES
+           : algo == WF16_LOCAL_TBD ? (R <= 12 ? 3 : kW16_LTBD_WAVES)   // G16R12: the 3-wave A/B shape
+           : algo == WF16_LOCAL_SEGR ? 2                                 // 2R more VGPRs than WF16_LOCAL_SEG
            : algo == WF16_LOCAL_K2 ? kW16_K2_WAVES
            : algo == WF16_SEMI_TQ ? (R > 20 ? kW16_TQ_BIG_WAVES : kW16_TQ_WAVES)
            : algo == WF16_GLOBAL_CP ? kW16_CP_WAVES

@@ -1351,3 +1351,37 @@ def test_tail_shape_declined_blocks(engine, monkeypatch, k_extra):
     assert total == n and n - 64 * len(picks) <= handled < n
     for f in ("score", "q_end", "t_end"):
         assert np.array_equal(g[f], o[f]), f
+
+
+def test_local_traceback_three_wave_shape(engine, monkeypatch):
+    """LOCAL+TB on the 3-wave G16R12 instance (GASALX_LTBD_G16=1, the A/B of VERDICT r05 item 4):
+    CIGAR bytes, n_ops, starts and ends as the oracle, config-2 data and ragged pairs."""
+    monkeypatch.setenv("GASALX_LTBD_G16", "1")
+    kw = dict(algo=G.LOCAL, start_pos=G.WITH_TB)
+    assert G.describe_plan(G.make_params(**kw), 150, 150).endswith("_G16R12")
+    check(engine, no_cigar_overflow(G.Batch.synth(2, 20000, 0x5EED0002), **kw), cigar=True, **kw)
+    rng = np.random.default_rng(0x16C12)
+    # (lengths inside the e-drift kernel's f16 key range, (Hmax + 1) * (C + 16) <= 0x7800)
+    qs, ts = helpers.random_pairs(rng, 900, 1, 150, 1, 180, alphabet=b"ACGTACGTN", related=0.6)
+    check(engine, no_cigar_overflow(G.Batch.from_pairs(qs, ts), **kw), cigar=True, **kw)
+
+
+def test_local_segments_in_registers(engine, monkeypatch):
+    """LOCAL keys by step segments with the finished segments' best per row in registers
+    (GASALX_KSEG_REG=1, WF16_LOCAL_SEGR, the A/B of VERDICT r05 item 6) on 300 x 300 pairs,
+    including maxima tied across segment boundaries (a later segment wins only when higher)."""
+    monkeypatch.setenv("GASALX_KSEG_REG", "1")
+    kw = dict(algo=G.LOCAL)
+    assert G.describe_plan(G.make_params(**kw), 300, 300) == "wavefront16_local_seg64_G16R20"
+    check(engine, G.Batch.synth(3, 30000, 0x5EED0003), **kw)
+    rng = np.random.default_rng(0x5E6)
+    rep = helpers.random_seq(rng, 50)
+    qs, ts = [], []
+    for i in range(400):
+        qs.append(helpers.random_seq(rng, 20 + i % 40) + rep + helpers.random_seq(rng, 30))
+        gap = 10 + (i * 7) % 150
+        ts.append(helpers.random_seq(rng, 5 + i % 60) + rep + helpers.random_seq(rng, gap) + rep +
+                  helpers.random_seq(rng, 8))
+    qs = [q[:300] for q in qs]
+    ts = [t[:300] for t in ts]
+    check(engine, G.Batch.from_pairs(qs, ts), **kw)

@@ -6,6 +6,7 @@
 // (include/gasal_header.h, -lgasal), like tools/test_prog.cpp.
 //
 //   boundary_bench [--repl N] [--batch B] [--storages S] [--warm W] [--reps K] [--dump FILE]
+//                  [--poll-us U (probe: sleep U us between polls once a thread's pairs are all launched)]
 //                  <test_prog options: -y local|semi_global|global|ksw|banded, -s, -t, -n T, ...>
 //                  query.fasta[.gz] target.fasta[.gz]
 //
@@ -20,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/time.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -67,7 +69,7 @@ struct Slot {
 }  // namespace
 
 int main(int argc, char **argv) {
-    int repl = 1, batch = 5000, storages = 2, warm = 1, reps = 3;
+    int repl = 1, batch = 5000, storages = 2, warm = 1, reps = 3, poll_us = 0;
     const char *dump = nullptr;
     std::vector<char *> rest = {argv[0]};
     for (int i = 1; i < argc; ++i) {
@@ -81,6 +83,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--warm")) warm = atoi(val("--warm"));
         else if (!strcmp(argv[i], "--reps")) reps = atoi(val("--reps"));
         else if (!strcmp(argv[i], "--dump")) dump = val("--dump");
+        else if (!strcmp(argv[i], "--poll-us")) poll_us = atoi(val("--poll-us"));   // probe: sleep between polls
         else rest.push_back(argv[i]);
     }
     if (rest.size() < 3) { fprintf(stderr, "usage: boundary_bench [options] query.fasta target.fasta\n"); return 1; }
@@ -134,6 +137,7 @@ int main(int argc, char **argv) {
             for (int z = 0; z < storages; ++z) slots[z].st = &vecs[tid].a[z];
             int next = begin, in_flight = 0;
             while (next < end || in_flight > 0) {
+                if (poll_us > 0 && next >= end) usleep(poll_us);
                 for (Slot &s : slots) {   // launch on every free storage (test_prog.cpp:265-330)
                     if (next >= end || s.n != 0 || s.st->is_free != 1) continue;
                     const int n = std::min(batch, end - next);
