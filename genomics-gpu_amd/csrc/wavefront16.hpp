@@ -80,6 +80,15 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 }
 
 constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
+#ifndef GX_LOCAL_FENCE
+#define GX_LOCAL_FENCE 0   // A/B: scheduling fences after the LOCAL sweep's table reads
+#endif
+#ifndef GX_LOCAL_IL2
+#define GX_LOCAL_IL2 1     // the LOCAL sweep's rows in interleaved pairs (+1.0 %, profiles/r06/ab)
+#endif
+#ifndef GX_LOCAL_ATIE
+#define GX_LOCAL_ATIE 1    // the LOCAL keys' scalar addends kept as a chain (with IL2: +2.4 %, profiles/r06/ab)
+#endif
 #ifndef GX_WF16_WAVES
 #define GX_WF16_WAVES 3   // waves per SIMD the register allocator must allow
 #endif
@@ -206,8 +215,54 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
     // row 0's addends (invp / invn: the candidates' bases), then one scalar subtract per row
     const uint32_t g20 = (FL[0] - EXT2) & 0xFFFFu, EM = (EXT2 >> 1 & 0xFFFFu) * MK16;   // e * M
     uint32_t a1 = invp - g20 * MK16, a2 = invn - g20 * MK16;
+#if GX_LOCAL_IL2
+    // A/B: two rows' independent parts interleaved (table byte, diagonal add, the two offsets), pinned
+    // stage by stage with empty asm ties, so that no instruction waits on the one just before it
+    constexpr int R2 = R & ~1;
+#pragma unroll
+    for (int k = 0; k < R2; k += 2) {
+        uint32_t v0 = __builtin_amdgcn_perm(T.y, T.x, xs[k]), v1 = __builtin_amdgcn_perm(T.y, T.x, xs[k + 1]);
+        asm volatile("" : "+v"(v0), "+v"(v1));
+        uint32_t t0 = pk_addnc(diag, v0), t1 = pk_addnc(Hin[k], v1);
+        asm volatile("" : "+v"(t0), "+v"(t1));
+        uint32_t tmp0 = pk_subnb(t0, KX), tmp1 = pk_subnb(t1, KX), toe0 = pk_subnb(t0, OEX), toe1 = pk_subnb(t1, OEX);
+        asm volatile("" : "+v"(tmp0), "+v"(tmp1), "+v"(toe0), "+v"(toe1));
+        const uint32_t H0 = pk_max3(tmp0, f, Ek[k]);
+        const uint32_t f1 = pk_max_u16(toe0, f);
+        Ek[k] = pk_max3(toe0, Ek[k], FL[k]);
+        const uint32_t H1 = pk_max3(tmp1, f1, Ek[k + 1]);
+        f = pk_max_u16(toe1, f1);
+        Ek[k + 1] = pk_max3(toe1, Ek[k + 1], FL[k + 1]);
+        if (KEYS) {
+            if (U16)
+                key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H0, KMUL, a2)));
+            else
+                key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H0, KMUL, a2));
+            a1 -= EM;
+            a2 -= EM;
+            if (U16)
+                key[k + 1] = pk_max_u16(key[k + 1], pk_max_u16(pk_mad_u16_lo(Hin[k + 1], KMUL, a1),
+                                                               pk_mad_u16_lo(H1, KMUL, a2)));
+            else
+                key[k + 1] = pk_max3(key[k + 1], pk_mad_u16_lo(Hin[k + 1], KMUL, a1), pk_mad_u16_lo(H1, KMUL, a2));
+            a1 -= EM;
+            a2 -= EM;
+#if GX_LOCAL_ATIE
+            asm volatile("" : "+s"(a1), "+s"(a2));
+#endif
+        }
+        FL[k] = pk_addnc(FL[k], EXT);
+        FL[k + 1] = pk_addnc(FL[k + 1], EXT);
+        diag = Hin[k + 1];
+        Hout[k] = H0;
+        Hout[k + 1] = H1;
+    }
+#pragma unroll
+    for (int k = R2; k < R; ++k) {
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
+#endif
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
         const uint32_t t1 = pk_addnc(diag, v);
         const uint32_t tmp = pk_subnb(t1, KX);
@@ -224,6 +279,11 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                 key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
             a1 -= EM;   // row k + 1: FL one e higher
             a2 -= EM;
+#if GX_LOCAL_ATIE
+            // keep the addends a chain of one subtract per row: left alone, the compiler rebuilt each
+            // row's from FL[k] (a subtract, a multiply and an add: 3 SALU per row instead of 1)
+            asm volatile("" : "+s"(a1), "+s"(a2));
+#endif
         }
         FL[k] = pk_addnc(FL[k], EXT);
         f = pk_max_u16(toe, f);
