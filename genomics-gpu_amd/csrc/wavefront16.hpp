@@ -86,6 +86,15 @@ constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_LOCAL_IL2
 #define GX_LOCAL_IL2 1     // the LOCAL sweep's rows in interleaved pairs (+1.0 %, profiles/r06/ab)
 #endif
+#ifndef GX_SEMI_IL2
+#define GX_SEMI_IL2 0      // A/B: the SEMI sweep's rows in interleaved pairs (-1.3 % on config 4)
+#endif
+#ifndef GX_GLOBAL_IL2
+#define GX_GLOBAL_IL2 1    // the GLOBAL sweep's rows in interleaved pairs (NW +1.4 %, config 3 +2-4 %)
+#endif
+#ifndef GX_TB_IL2
+#define GX_TB_IL2 1        // the traceback sweeps' rows in interleaved pairs (LOCAL+TB +0.7 %)
+#endif
 #ifndef GX_LOCAL_ATIE
 #define GX_LOCAL_ATIE 1    // the LOCAL keys' scalar addends kept as a chain (with IL2: +2.4 %, profiles/r06/ab)
 #endif
@@ -311,8 +320,33 @@ __device__ __forceinline__ void step_global(const uint2 T, const uint32_t diag_t
                                             uint32_t (&Ek)[R], uint32_t &f_out, const uint32_t KX,
                                             const uint32_t OEX, const uint32_t NN) {
     uint32_t diag = diag_top, f = f_top;
+#if GX_GLOBAL_IL2
+    constexpr int R2 = R & ~1;
+#pragma unroll
+    for (int k = 0; k < R2; k += 2) {
+        uint32_t v0 = __builtin_amdgcn_perm(T.y, T.x, xs[k]), v1 = __builtin_amdgcn_perm(T.y, T.x, xs[k + 1]);
+        asm volatile("" : "+v"(v0), "+v"(v1));
+        uint32_t t0 = pk_addnc(diag, v0), t1 = pk_addnc(Hin[k], v1);
+        asm volatile("" : "+v"(t0), "+v"(t1));
+        uint32_t tmp0 = pk_subnb(t0, KX), tmp1 = pk_subnb(t1, KX), toe0 = pk_subnb(t0, OEX), toe1 = pk_subnb(t1, OEX);
+        asm volatile("" : "+v"(tmp0), "+v"(tmp1), "+v"(toe0), "+v"(toe1));
+        const uint32_t H0 = pk_max3(tmp0, f, Ek[k]);
+        Ek[k] = pk_max3(toe0, Ek[k], NN);
+        const uint32_t f1 = pk_max3(toe0, f, NN);
+        const uint32_t H1 = pk_max3(tmp1, f1, Ek[k + 1]);
+        Ek[k + 1] = pk_max3(toe1, Ek[k + 1], NN);
+        f = pk_max3(toe1, f1, NN);
+        diag = Hin[k + 1];
+        Hout[k] = H0;
+        Hout[k + 1] = H1;
+        if (SYNC) asm volatile("" : "+v"(Ek[k]), "+v"(Ek[k + 1]), "+v"(f));
+    }
+#pragma unroll
+    for (int k = R2; k < R; ++k) {
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
+#endif
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
         const uint32_t t1 = pk_addnc(diag, v);
         const uint32_t tmp = pk_subnb(t1, KX);
@@ -375,6 +409,46 @@ __device__ __forceinline__ void step_local_tb_dr(const uint2 T, const uint32_t d
     // floors in scalar registers overflowed them at this kernel's two waves (readlane spills)
     const uint32_t g20 = (FL0 - EXT2) & 0xFFFFu, EM = ((EXT2 >> 1) & 0xFFFFu) * MK16;
     uint32_t a1 = invp - g20 * MK16, a2 = invn - g20 * MK16, flk = FL0;
+    auto cell = [&](const int k, const uint32_t tmp, const uint32_t toe) __attribute__((always_inline)) {
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        const uint32_t En = pk_max3(toe, Ek[k], flk);
+        const uint32_t Fn = pk_max_u16(toe, f);
+        const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, Ek[k]), fy = tb_flag(toe, f);
+        const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
+        const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
+        dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
+        if (KEYS) {
+            key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
+            a1 -= EM;
+            a2 -= EM;
+        }
+        flk = pk_addnc(flk, EXT);
+        Ek[k] = En;
+        f = Fn;
+        Hout[k] = H;
+        if (KEYS) asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(a1), "+s"(a2), "+s"(flk));
+        else asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(flk));
+    };
+#if GX_TB_IL2
+    constexpr int R2 = R & ~1;
+#pragma unroll
+    for (int k = 0; k < R2; k += 2) {
+        uint32_t v0 = __builtin_amdgcn_perm(T.y, T.x, xs[k]), v1 = __builtin_amdgcn_perm(T.y, T.x, xs[k + 1]);
+        asm volatile("" : "+v"(v0), "+v"(v1));
+        uint32_t t0 = pk_addnc(diag, v0), t1 = pk_addnc(Hin[k], v1);
+        asm volatile("" : "+v"(t0), "+v"(t1));
+        uint32_t tmp0 = pk_subnb(t0, KX), tmp1 = pk_subnb(t1, KX), toe0 = pk_subnb(t0, OEX), toe1 = pk_subnb(t1, OEX);
+        asm volatile("" : "+v"(tmp0), "+v"(tmp1), "+v"(toe0), "+v"(toe1));
+        cell(k, tmp0, toe0);
+        cell(k + 1, tmp1, toe1);
+        diag = Hin[k + 1];
+    }
+    if (R & 1) {
+        constexpr int k = R - 1;
+        const uint32_t t1 = pk_addnc(diag, __builtin_amdgcn_perm(T.y, T.x, xs[k]));
+        cell(k, pk_subnb(t1, KX), pk_subnb(t1, OEX));
+    }
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
@@ -402,6 +476,7 @@ __device__ __forceinline__ void step_local_tb_dr(const uint2 T, const uint32_t d
         if (KEYS) asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(a1), "+s"(a2), "+s"(flk));
         else asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(flk));
     }
+#endif
     FL0 = pk_addnc(FL0, EXT);   // the next step
     f_out = f;
 }
@@ -414,6 +489,40 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
                                                const uint32_t NN, const int j) {
     const uint32_t M1 = 0x01010101u << j, M2 = 0x10101010u << j;
     uint32_t diag = diag_top, f = f_top, tx = T.x, ty = T.y;
+#if GX_TB_IL2
+    auto cell = [&](const int k, const uint32_t tmp, const uint32_t toe) __attribute__((always_inline)) {
+        const uint32_t H = pk_max3(tmp, f, Ek[k]);
+        const uint32_t em = Ek[k], fm = f;
+        const uint32_t En = pk_max3(toe, em, NN);
+        const uint32_t Fn = pk_max3(toe, fm, NN);
+        const uint32_t fu = tb_flag(H, tmp), fw = tb_flag(H, f), fx = tb_flag(toe, em), fy = tb_flag(toe, fm);
+        const uint32_t m1 = __builtin_amdgcn_perm(fx, fu, 0x0B090A08u);
+        const uint32_t m2 = __builtin_amdgcn_perm(fy, fw, 0x0B090A08u);
+        dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
+        Ek[k] = En;
+        f = Fn;
+        Hout[k] = H;
+        if (SYNC) asm volatile("" : "+v"(dw[k]), "+v"(f));
+    };
+    constexpr int R2 = R & ~1;
+#pragma unroll
+    for (int k = 0; k < R2; k += 2) {
+        uint32_t v0 = __builtin_amdgcn_perm(ty, tx, xs[k]), v1 = __builtin_amdgcn_perm(ty, tx, xs[k + 1]);
+        asm volatile("" : "+v"(v0), "+v"(v1));
+        uint32_t t0 = pk_addnc(diag, v0), t1 = pk_addnc(Hin[k], v1);
+        asm volatile("" : "+v"(t0), "+v"(t1));
+        uint32_t tmp0 = pk_subnb(t0, KX), tmp1 = pk_subnb(t1, KX), toe0 = pk_subnb(t0, OEX), toe1 = pk_subnb(t1, OEX);
+        asm volatile("" : "+v"(tmp0), "+v"(tmp1), "+v"(toe0), "+v"(toe1));
+        cell(k, tmp0, toe0);
+        cell(k + 1, tmp1, toe1);
+        diag = Hin[k + 1];
+    }
+    if (R & 1) {
+        constexpr int k = R - 1;
+        const uint32_t t1 = pk_addnc(diag, __builtin_amdgcn_perm(ty, tx, xs[k]));
+        cell(k, pk_subnb(t1, KX), pk_subnb(t1, OEX));
+    }
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
         const uint32_t v = __builtin_amdgcn_perm(ty, tx, xs[k]);
@@ -437,6 +546,7 @@ __device__ __forceinline__ void step_global_tb(const uint2 T, const uint32_t dia
         // window's store otherwise: 345 spilled VGPRs; 120 VGPRs with it)
         if (SYNC) asm volatile("" : "+v"(dw[k]), "+v"(f));
     }
+#endif
     f_out = f;
 }
 
@@ -500,8 +610,33 @@ __device__ __forceinline__ void step_semi(const uint2 T, const uint32_t diag_top
                                           const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                           uint32_t (&Fk)[R], const uint32_t GO, const uint32_t *pv = nullptr) {
     uint32_t diag = diag_top, h = hl, e = el;
+#if GX_SEMI_IL2
+    constexpr int R2 = R & ~1;
+#pragma unroll
+    for (int k = 0; k < R2; k += 2) {
+        uint32_t v0 = __builtin_amdgcn_perm(T.y, T.x, xs[k]), v1 = __builtin_amdgcn_perm(T.y, T.x, xs[k + 1]);
+        if (PV > 0 && k >= R - PV) v0 = pk_addnc(v0, pv[k - (R - PV)]);
+        if (PV > 0 && k + 1 >= R - PV) v1 = pk_addnc(v1, pv[k + 1 - (R - PV)]);
+        asm volatile("" : "+v"(v0), "+v"(v1));
+        uint32_t t0 = pk_addnc(diag, v0), t1 = pk_addnc(Hin[k], v1);
+        uint32_t F0 = pk_max_u16(Hin[k], Fk[k]), F1 = pk_max_u16(Hin[k + 1], Fk[k + 1]);
+        asm volatile("" : "+v"(t0), "+v"(t1), "+v"(F0), "+v"(F1));
+        e = pk_max_u16(h, e);
+        h = pk_subnb(pk_max3(t0, F0, e), GO);
+        Hout[k] = h;
+        e = pk_max_u16(h, e);
+        h = pk_subnb(pk_max3(t1, F1, e), GO);
+        Hout[k + 1] = h;
+        Fk[k] = F0;
+        Fk[k + 1] = F1;
+        diag = Hin[k + 1];
+    }
+#pragma unroll
+    for (int k = R2; k < R; ++k) {
+#else
 #pragma unroll
     for (int k = 0; k < R; ++k) {
+#endif
         uint32_t v = __builtin_amdgcn_perm(T.y, T.x, xs[k]);
         if (PV > 0 && k >= R - PV) v = pk_addnc(v, pv[k - (R - PV)]);
         const uint32_t tmp = pk_addnc(diag, v);                     // H(r-1,c-1) + s
