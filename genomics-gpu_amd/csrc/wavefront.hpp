@@ -92,8 +92,11 @@ constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = 64 * kWavesPerBlock;
 constexpr uint8_t kInvalidCode = 0xFF;
 
-__device__ __forceinline__ int32_t shr_lane(int32_t v) {   // lane i <- lane i-1
-    return __builtin_amdgcn_update_dpp(0, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, false);
+#ifndef GX_DPP_FUSE
+#define GX_DPP_FUSE 1   // bound_ctrl hand-offs (no "old" init; a following subtract folds into the DPP op): +0.6 %
+#endif
+__device__ __forceinline__ int32_t shr_lane(int32_t v) {   // lane i <- lane i-1 (lane 0 <- 0)
+    return __builtin_amdgcn_update_dpp(0, v, 0x138 /* wave_shr:1 */, 0xF, 0xF, GX_DPP_FUSE != 0);
 }
 
 __device__ __forceinline__ int32_t max3(int32_t a, int32_t b, int32_t c) {

@@ -95,6 +95,9 @@ constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_TB_IL2
 #define GX_TB_IL2 1        // the traceback sweeps' rows in interleaved pairs (LOCAL+TB +0.7 %)
 #endif
+#ifndef GX_CP_ST16
+#define GX_CP_ST16 0       // A/B: the config-3 sweep's checkpoint and stream stores 16 bytes wide
+#endif
 #ifndef GX_LOCAL_ATIE
 #define GX_LOCAL_ATIE 1    // the LOCAL keys' scalar addends kept as a chain (with IL2: +2.4 %, profiles/r06/ab)
 #endif
