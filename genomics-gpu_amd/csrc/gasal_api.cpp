@@ -57,41 +57,91 @@ template <class T> void dev_alloc(T **p, size_t count) {
     CHECKHIPERROR(hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
     CHECKHIPERROR(hipMemset(*p, 0, std::max<size_t>(count, 1) * sizeof(T)));
 }
-template <class T> void host_free(T *&p) { if (p) CHECKHIPERROR(hipHostFree(p)); p = nullptr; }
-template <class T> void dev_free(T *&p) { if (p) CHECKHIPERROR(hipFree(p)); p = nullptr; }
+
+// Arrays of one storage that travel together (the four lens/offsets arrays, the result arrays)
+// live in one allocation, `cap` elements apart, so that a batch moves them with one copy instead
+// of one per array (each hipMemcpyAsync is a DMA command of its own: the boundary bench's 5,000-
+// pair batches spent more engine time on the small copies than on their bytes).  The arrays
+// keep their own pointers (the reference's fields); the block is freed with its last array.
+struct Block { void *base; size_t cap; int refs; bool dev; };
+std::mutex g_bmu;
+std::map<const void *, Block *> g_blk;   // every array pointer of a block -> its block
+
+template <class T> void block_alloc(bool dev, size_t cap, std::initializer_list<T **> arrays) {
+    cap = std::max<size_t>(cap, 1);
+    T *base = nullptr;
+    if (dev) dev_alloc(&base, cap * arrays.size());
+    else host_alloc(&base, cap * arrays.size());
+    Block *b = new Block{base, cap, (int)arrays.size(), dev};
+    std::lock_guard<std::mutex> lk(g_bmu);
+    size_t i = 0;
+    for (T **a : arrays) { *a = base + cap * i++; g_blk[*a] = b; }
+}
+// true when p was an array of a block (released; the block freed with its last array)
+bool block_release(const void *p) {
+    Block *b = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_bmu);
+        auto it = g_blk.find(p);
+        if (it == g_blk.end()) return false;
+        b = it->second;
+        g_blk.erase(it);
+        if (--b->refs > 0) return true;
+    }
+    if (b->dev) CHECKHIPERROR(hipFree(b->base));
+    else CHECKHIPERROR(hipHostFree(b->base));
+    delete b;
+    return true;
+}
+// elements per array when a[0..k) are consecutive arrays of one block, else 0
+template <class T> size_t block_run(std::initializer_list<T *> a) {
+    std::lock_guard<std::mutex> lk(g_bmu);
+    const T *first = *a.begin();
+    auto it = g_blk.find(first);
+    if (it == g_blk.end()) return 0;
+    const size_t cap = it->second->cap;
+    size_t i = 0;
+    for (T *p : a) {
+        auto jt = g_blk.find(p);
+        if (jt == g_blk.end() || jt->second != it->second || p != first + cap * i) return 0;
+        ++i;
+    }
+    return cap;
+}
+
+template <class T> void host_free(T *&p) { if (p && !block_release(p)) CHECKHIPERROR(hipHostFree(p)); p = nullptr; }
+template <class T> void dev_free(T *&p) { if (p && !block_release(p)) CHECKHIPERROR(hipFree(p)); p = nullptr; }
 
 uint32_t pad8(uint32_t x) { return x % 8 ? x + (8 - x % 8) : x; }
 
 }  // namespace
 
 // ============================================================== res.cpp ====
+// the result arrays in one block per side, in the order score, q_end, t_end, q_start, t_start
+// (the fields res.cpp:26-67 / :115-138 allocate), so gasal_aln_async returns them with one copy
+static void res_block(bool dev, uint32_t max_n_alns, Parameters *params, gasal_res_t *res) {
+    const bool ends = params->algo != GLOBAL;
+    const bool starts = ends && (params->start_pos == WITH_START || params->start_pos == WITH_TB);
+    if (starts)
+        block_alloc<int32_t>(dev, max_n_alns, {&res->aln_score, &res->query_batch_end, &res->target_batch_end,
+                                               &res->query_batch_start, &res->target_batch_start});
+    else if (ends)
+        block_alloc<int32_t>(dev, max_n_alns, {&res->aln_score, &res->query_batch_end, &res->target_batch_end});
+    else
+        block_alloc<int32_t>(dev, max_n_alns, {&res->aln_score});
+}
+
 gasal_res_t *gasal_res_new_host(uint32_t max_n_alns, Parameters *params) {
     gasal_res_t *res = (gasal_res_t *)calloc(1, sizeof(gasal_res_t));
     if (!res) { fprintf(stderr, "Malloc error on res host "); exit(1); }
-    host_alloc(&res->aln_score, max_n_alns);
-    if (params->algo != GLOBAL) {                                   // res.cpp:26-67
-        if (params->start_pos == WITH_START || params->start_pos == WITH_TB) {
-            host_alloc(&res->query_batch_start, max_n_alns);
-            host_alloc(&res->target_batch_start, max_n_alns);
-        }
-        host_alloc(&res->query_batch_end, max_n_alns);
-        host_alloc(&res->target_batch_end, max_n_alns);
-    }
+    res_block(false, max_n_alns, params, res);
     if (params->start_pos == WITH_TB) host_alloc(&res->n_cigar_ops, max_n_alns);   // :68-70
     return res;
 }
 
 gasal_res_t *gasal_res_new_device_cpy(uint32_t max_n_alns, Parameters *params) {
     gasal_res_t *res = (gasal_res_t *)calloc(1, sizeof(gasal_res_t));
-    dev_alloc(&res->aln_score, max_n_alns);
-    if (params->algo != GLOBAL) {                                   // res.cpp:115-138
-        if (params->start_pos == WITH_START || params->start_pos == WITH_TB) {
-            dev_alloc(&res->query_batch_start, max_n_alns);
-            dev_alloc(&res->target_batch_start, max_n_alns);
-        }
-        dev_alloc(&res->query_batch_end, max_n_alns);
-        dev_alloc(&res->target_batch_end, max_n_alns);
-    }
+    res_block(true, max_n_alns, params, res);
     return res;
 }
 
@@ -267,10 +317,24 @@ void gasal_host_alns_resize(gasal_gpu_storage_t *gs, int new_max_alns, Parameter
     gs->host_query_op = host_realloc(gs->host_query_op, new_max_alns, gs->host_max_n_alns);
     gs->host_target_op = host_realloc(gs->host_target_op, new_max_alns, gs->host_max_n_alns);
     if (params->algo == KSW) gs->host_seed_scores = host_realloc(gs->host_seed_scores, new_max_alns, gs->host_max_n_alns);
-    gs->host_query_batch_lens = host_realloc(gs->host_query_batch_lens, new_max_alns, gs->host_max_n_alns);
-    gs->host_target_batch_lens = host_realloc(gs->host_target_batch_lens, new_max_alns, gs->host_max_n_alns);
-    gs->host_query_batch_offsets = host_realloc(gs->host_query_batch_offsets, new_max_alns, gs->host_max_n_alns);
-    gs->host_target_batch_offsets = host_realloc(gs->host_target_batch_offsets, new_max_alns, gs->host_max_n_alns);
+    {
+        // the four lens / offsets arrays move to a new block together (contents kept, as cudaHostRealloc)
+        uint32_t *ql = gs->host_query_batch_lens, *tl = gs->host_target_batch_lens;
+        uint32_t *qo = gs->host_query_batch_offsets, *to = gs->host_target_batch_offsets;
+        if (new_max_alns < (int)gs->host_max_n_alns) {
+            fprintf(stderr, "[GASAL ERROR] cudoHostRealloc: invalid sizes. New size < old size (%d < %d)", new_max_alns,
+                    gs->host_max_n_alns);
+            exit(EXIT_FAILURE);
+        }
+        block_alloc<uint32_t>(false, new_max_alns, {&gs->host_query_batch_lens, &gs->host_target_batch_lens,
+                                                    &gs->host_query_batch_offsets, &gs->host_target_batch_offsets});
+        const size_t old_bytes = (size_t)gs->host_max_n_alns * 4;
+        std::memcpy(gs->host_query_batch_lens, ql, old_bytes);
+        std::memcpy(gs->host_target_batch_lens, tl, old_bytes);
+        std::memcpy(gs->host_query_batch_offsets, qo, old_bytes);
+        std::memcpy(gs->host_target_batch_offsets, to, old_bytes);
+        host_free(ql); host_free(tl); host_free(qo); host_free(to);
+    }
     uint8_t *cigar = gs->host_res ? gs->host_res->cigar : nullptr;
     if (gs->host_res) gs->host_res->cigar = nullptr;
     gasal_res_destroy_host(gs->host_res);
@@ -363,14 +427,10 @@ void gasal_init_streams(gasal_gpu_storage_v *vec, int max_query_len, int max_tar
             gs->host_seed_scores = NULL;
             gs->seed_scores = NULL;
         }
-        host_alloc(&gs->host_query_batch_lens, max_n_alns);
-        host_alloc(&gs->host_target_batch_lens, max_n_alns);
-        host_alloc(&gs->host_query_batch_offsets, max_n_alns);
-        host_alloc(&gs->host_target_batch_offsets, max_n_alns);
-        dev_alloc(&gs->query_batch_lens, max_n_alns);
-        dev_alloc(&gs->target_batch_lens, max_n_alns);
-        dev_alloc(&gs->query_batch_offsets, max_n_alns);
-        dev_alloc(&gs->target_batch_offsets, max_n_alns);
+        block_alloc<uint32_t>(false, max_n_alns, {&gs->host_query_batch_lens, &gs->host_target_batch_lens,
+                                                  &gs->host_query_batch_offsets, &gs->host_target_batch_offsets});
+        block_alloc<uint32_t>(true, max_n_alns, {&gs->query_batch_lens, &gs->target_batch_lens,
+                                                 &gs->query_batch_offsets, &gs->target_batch_offsets});
         gs->host_res = gasal_res_new_host(max_n_alns, params);
         if (params->start_pos == WITH_TB) host_alloc(&gs->host_res->cigar, qbytes);
         gs->device_cpy = gasal_res_new_device_cpy(max_n_alns, params);
@@ -451,10 +511,8 @@ void gasal_gpu_mem_alloc(gasal_gpu_storage_t *gs, int qb, int tb, int na, Parame
     dev_alloc(&gs->unpacked_target_batch, tb);
     dev_alloc(&gs->packed_query_batch, qb / 8);
     dev_alloc(&gs->packed_target_batch, tb / 8);
-    dev_alloc(&gs->query_batch_lens, na);
-    dev_alloc(&gs->target_batch_lens, na);
-    dev_alloc(&gs->query_batch_offsets, na);
-    dev_alloc(&gs->target_batch_offsets, na);
+    block_alloc<uint32_t>(true, na, {&gs->query_batch_lens, &gs->target_batch_lens, &gs->query_batch_offsets,
+                                     &gs->target_batch_offsets});
     if (!gs->device_cpy) gs->device_cpy = gasal_res_new_device_cpy(na, params);
     gs->device_res = gasal_res_new_device(gs->device_cpy);
     gs->gpu_max_query_batch_bytes = qb;
@@ -545,10 +603,8 @@ void gasal_aln_async(gasal_gpu_storage_t *gs, const uint32_t qbytes, const uint3
             dev_free(*p);
         dev_free(gs->query_op);
         dev_free(gs->target_op);
-        dev_alloc(&gs->query_batch_lens, gs->gpu_max_n_alns);
-        dev_alloc(&gs->target_batch_lens, gs->gpu_max_n_alns);
-        dev_alloc(&gs->query_batch_offsets, gs->gpu_max_n_alns);
-        dev_alloc(&gs->target_batch_offsets, gs->gpu_max_n_alns);
+        block_alloc<uint32_t>(true, gs->gpu_max_n_alns, {&gs->query_batch_lens, &gs->target_batch_lens,
+                                                         &gs->query_batch_offsets, &gs->target_batch_offsets});
         dev_alloc(&gs->seed_scores, gs->gpu_max_n_alns);
         dev_alloc(&gs->query_op, gs->gpu_max_n_alns);
         dev_alloc(&gs->target_op, gs->gpu_max_n_alns);
@@ -568,10 +624,19 @@ void gasal_aln_async(gasal_gpu_storage_t *gs, const uint32_t qbytes, const uint3
     for (host_batch_t *p = gs->extensible_host_unpacked_target_batch; p; p = p->next)
         if (p->data_size) CHECKHIPERROR(hipMemcpyAsync(gs->unpacked_target_batch + p->offset, p->data, p->data_size, hipMemcpyHostToDevice, st));
     // lens / offsets / seeds / ops (:207-235)
-    CHECKHIPERROR(hipMemcpyAsync(gs->query_batch_lens, gs->host_query_batch_lens, n * 4ull, hipMemcpyHostToDevice, st));
-    CHECKHIPERROR(hipMemcpyAsync(gs->target_batch_lens, gs->host_target_batch_lens, n * 4ull, hipMemcpyHostToDevice, st));
-    CHECKHIPERROR(hipMemcpyAsync(gs->query_batch_offsets, gs->host_query_batch_offsets, n * 4ull, hipMemcpyHostToDevice, st));
-    CHECKHIPERROR(hipMemcpyAsync(gs->target_batch_offsets, gs->host_target_batch_offsets, n * 4ull, hipMemcpyHostToDevice, st));
+    const size_t mcap_h = block_run<uint32_t>({gs->host_query_batch_lens, gs->host_target_batch_lens,
+                                               gs->host_query_batch_offsets, gs->host_target_batch_offsets});
+    const size_t mcap_d = block_run<uint32_t>({gs->query_batch_lens, gs->target_batch_lens, gs->query_batch_offsets,
+                                               gs->target_batch_offsets});
+    if (mcap_h && mcap_h == mcap_d) {   // one copy: three whole arrays and the first n of the fourth
+        CHECKHIPERROR(hipMemcpyAsync(gs->query_batch_lens, gs->host_query_batch_lens, (3 * mcap_h + n) * 4ull,
+                                     hipMemcpyHostToDevice, st));
+    } else {
+        CHECKHIPERROR(hipMemcpyAsync(gs->query_batch_lens, gs->host_query_batch_lens, n * 4ull, hipMemcpyHostToDevice, st));
+        CHECKHIPERROR(hipMemcpyAsync(gs->target_batch_lens, gs->host_target_batch_lens, n * 4ull, hipMemcpyHostToDevice, st));
+        CHECKHIPERROR(hipMemcpyAsync(gs->query_batch_offsets, gs->host_query_batch_offsets, n * 4ull, hipMemcpyHostToDevice, st));
+        CHECKHIPERROR(hipMemcpyAsync(gs->target_batch_offsets, gs->host_target_batch_offsets, n * 4ull, hipMemcpyHostToDevice, st));
+    }
     if (params->algo == KSW) {
         if (gs->seed_scores == NULL) fprintf(stderr, "seed_scores == NULL\n");
         if (gs->host_seed_scores == NULL) fprintf(stderr, "host_seed_scores == NULL\n");
@@ -636,14 +701,34 @@ void gasal_aln_async(gasal_gpu_storage_t *gs, const uint32_t qbytes, const uint3
 #define D2H(field)                                                                                          \
     if (h->field != NULL && d->field != NULL)                                                               \
         CHECKHIPERROR(hipMemcpyAsync(h->field, d->field, n * sizeof(*h->field), hipMemcpyDeviceToHost, st));
-    D2H(aln_score) D2H(query_batch_start) D2H(target_batch_start) D2H(query_batch_end) D2H(target_batch_end)
+    // one copy when both sides hold the same result arrays in one block of the same capacity
+    auto res_d2h = [&](gasal_res_t *h, gasal_res_t *d) {
+        const bool st5 = h->query_batch_start && d->query_batch_start, e3 = h->query_batch_end && d->query_batch_end;
+        size_t ch = 0, cd = 0, k = 1;
+        if (st5) {
+            k = 5;
+            ch = block_run<int32_t>({h->aln_score, h->query_batch_end, h->target_batch_end, h->query_batch_start, h->target_batch_start});
+            cd = block_run<int32_t>({d->aln_score, d->query_batch_end, d->target_batch_end, d->query_batch_start, d->target_batch_start});
+        } else if (e3 && !h->query_batch_start && !d->query_batch_start) {
+            k = 3;
+            ch = block_run<int32_t>({h->aln_score, h->query_batch_end, h->target_batch_end});
+            cd = block_run<int32_t>({d->aln_score, d->query_batch_end, d->target_batch_end});
+        } else if (!h->query_batch_end && !d->query_batch_end && !h->query_batch_start && !d->query_batch_start) {
+            ch = cd = n;   // the score alone
+        }
+        if (ch && ch == cd && h->aln_score && d->aln_score) {
+            CHECKHIPERROR(hipMemcpyAsync(h->aln_score, d->aln_score, ((k - 1) * ch + n) * 4ull, hipMemcpyDeviceToHost, st));
+            return;
+        }
+        D2H(aln_score) D2H(query_batch_start) D2H(target_batch_start) D2H(query_batch_end) D2H(target_batch_end)
+    };
+    res_d2h(h, d);
     if (params->start_pos == WITH_TB) {
         CHECKHIPERROR(hipMemcpyAsync(h->cigar, gs->unpacked_query_batch, qbytes, hipMemcpyDeviceToHost, st));
         CHECKHIPERROR(hipMemcpyAsync(h->n_cigar_ops, gs->query_batch_lens, n * 4ull, hipMemcpyDeviceToHost, st));
     }
     if (params->secondBest) {
-        h = gs->host_res_second; d = gs->device_cpy_second;
-        D2H(aln_score) D2H(query_batch_start) D2H(target_batch_start) D2H(query_batch_end) D2H(target_batch_end)
+        res_d2h(gs->host_res_second, gs->device_cpy_second);
     }
 #undef D2H
     gs->is_free = 0;
