@@ -227,6 +227,10 @@ static bool env_flag(const char *name, bool dflt) {
     const char *e = std::getenv(name);
     return e ? std::atoi(e) != 0 : dflt;
 }
+static int env_int(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
 
 // Packed banded kernel (banded16.hpp): stored values B + [0, Hmax] and keys
 // H*8 + 7 + 0x400 inside [0x0400, 0x7BFF]; pads score -b, which needs an N score
@@ -486,6 +490,7 @@ static hipError_t copy_d2d(void *dst, const void *src, size_t bytes, hipStream_t
 // GASALX_TAIL=0: one shape (A/B).
 struct TailShape {
     WfFn fn = nullptr;
+    int G2 = 0, R2 = 0;
     uint32_t b0 = 0, p0 = 0, ppb = 1, lds_stride = 0;
     size_t lds_bytes = 0;
     int32_t vmin = 0;   // GLOBAL: the value-window bound for the larger span of the two shapes
@@ -496,13 +501,21 @@ static TailShape tail_shape(const Plan &pl, const gasalx_params &p, const WfArgs
     const bool on = env_flag("GASALX_TAIL", true);
     const char *ke = std::getenv("GASALX_TAIL_K");
     const int kextra = ke ? std::atoi(ke) : 0;
-    if (!on || !pl.packed16 || pl.tb || pl.key2 || pl.ku16 || pl.kseg_shift || pl.semi_tq || A.rev || A.n_dev ||
-        A.stop || A.lstop)
+    if (!on || !pl.packed16 || (pl.tb && !pl.tb_band) || pl.key2 || pl.ku16 || pl.kseg_shift || pl.semi_tq ||
+        A.rev || A.n_dev || A.stop || A.lstop)
         return t;
     int G2 = 0, R2 = 0;
     WfFn fn = nullptr;
     if (pl.wf_algo == WF_LOCAL && pl.kf16 && pl.G16 == 8 && pl.R16 == 19) {
         G2 = 32; R2 = 5; fn = &wf16_mix_kernel<WF_LOCAL, 8, 19, 32, 5>;
+    } else if (pl.tb_band) {
+        // the band traceback's sweep + band pass (R % 4 == 0 for the band windows); GASALX_CP_TAIL=32: G32R12
+        if (pl.wf_algo != WF_GLOBAL || pl.G16 != 16 || pl.R16 != 20) return t;
+        if (env_int("GASALX_CP_TAIL", 64) == 32) {
+            G2 = 32; R2 = 12; fn = &wf16_mix_kernel<WF16_GLOBAL_CP, 16, 20, 32, 12>;
+        } else {
+            G2 = 64; R2 = 8; fn = &wf16_mix_kernel<WF16_GLOBAL_CP, 16, 20, 64, 8>;
+        }
     } else if (pl.wf_algo == WF_GLOBAL && pl.G16 == 16 && pl.R16 == 20) {
         G2 = 64; R2 = 5; fn = &wf16_mix_kernel<WF_GLOBAL, 16, 20, 64, 5>;
     } else {
@@ -540,6 +553,8 @@ static TailShape tail_shape(const Plan &pl, const gasalx_params &p, const WfArgs
     t.lds_stride = words * 8;
     t.lds_bytes = (size_t)kWavesPerBlock * (64 / G2) * t.lds_stride;
     t.fn = fn;
+    t.G2 = G2;
+    t.R2 = R2;
     return t;
 }
 
@@ -961,18 +976,30 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         A.tb_q8 = (pl.packed16 && pl.tb && !pl.tb_band && !A.perm) ? 1u : 0u;
         tb_q8 = A.tb_q8;
         if (pl.tb_band && runs_tb) {
-            // band recomputation buffers per wave of the packed launch (wavefront16.hpp)
+            // band recomputation buffers per wave of the packed launch (wavefront16.hpp); a mixed-
+            // shape launch (tail_shape) keeps its second region's after the first's
             const uint32_t ppb16 = kWavesPerBlock * (64 / pl.G16) * 2;
-            const uint64_t waves = (uint64_t)grid_for(n, ppb16) * kWavesPerBlock;
-            HIPCHK(ws.band_cp.reserve(waves * 2 * pl.R16 * 64 * 4 + 64));
-            HIPCHK(ws.band_stm.reserve(waves * 64 * band_stream_words(pl.band_wd) * 8 + 64));
-            HIPCHK(ws.band_fl.reserve(waves * 64 * (pl.band_wd / 4) * (pl.R16 / 4) * 16 + 64));
+            A.n = n;
+            const TailShape tail = tail_shape(pl, p, A, n);
+            const uint64_t waves = (uint64_t)(tail.fn ? tail.b0 : grid_for(n, ppb16)) * kWavesPerBlock;
+            const uint64_t waves2 = tail.fn ? (uint64_t)grid_for(n - tail.p0, tail.ppb) * kWavesPerBlock : 0;
+            const uint32_t wd2 = tail.fn ? (((uint32_t)(tail.R2 + 2 * pl.band_w) + 3u) & ~3u) : 4u;
+            const uint64_t cpw1 = waves * 2 * pl.R16 * 64, cpw2 = waves2 * 2 * tail.R2 * 64;   // words
+            const uint64_t st1 = waves * 64 * band_stream_words(pl.band_wd), st2 = waves2 * 64 * band_stream_words(wd2);
+            const uint64_t fl1 = waves * 64 * (pl.band_wd / 4) * (pl.R16 / 4), fl2 = waves2 * 64 * (wd2 / 4) * (tail.R2 / 4);
+            HIPCHK(ws.band_cp.reserve((cpw1 + cpw2) * 4 + 64));
+            HIPCHK(ws.band_stm.reserve((st1 + st2) * 8 + 64));
+            HIPCHK(ws.band_fl.reserve((fl1 + fl2) * 16 + 64));
             HIPCHK(ws.band_fb.reserve((size_t)n * 4 + grid_for(n, ppb16) + 256));
             A.cp = ws.band_cp.as<uint32_t>();
             A.stm = ws.band_stm.as<uint2>();
             A.bflags = ws.band_fl.as<uint4>();
             A.band_w = pl.band_w;
             A.band_wd = pl.band_wd;
+            A.cp2 = A.cp + cpw1;
+            A.stm2 = A.stm + st1;
+            A.bflags2 = A.bflags + fl1;
+            A.band_wd2 = wd2;
             fb_count = ws.band_fb.as<uint32_t>();
         }
         int rc = pl.semi_tq ? launch_semi_tq(ws, pl, p, A, st, shape.one_t8) : launch_wavefront(ws, pl, p, A, st);
@@ -1162,6 +1189,8 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         T.pk_flags = nullptr;
         T.pk_ppb = 1; T.pk_R = 1; T.pk_G = 1; T.pk_rmagic = 0; T.pk_q8 = 0;
         T.pk_fix = nullptr;
+        T.pk_p1 = 0xFFFFFFFFu; T.pk_b1 = 0; T.pk_ppb2 = 1;
+        T.band2 = nullptr; T.band_wd2 = 4; T.pk_R2 = 4; T.pk_G2 = 1; T.pk_ppw2 = 1; T.pk_rmagic2 = 0;
         T.slot_of = slot_of;
         T.sc_nn = p.has_n_penalty ? -p.n_penalty : p.match;   // GLOBAL: N == N is a match unless N_PENALTY
         T.qseq = qsrc; T.tseq = tsrc; T.toff = b.t_offsets; T.seq_packed = packed;
@@ -1175,6 +1204,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.pk_rmagic = (uint32_t)((0x100000000ull + pl.R16 - 1) / pl.R16);
             T.pk_fix = ws.aux.as<int32_t>();
             T.pk_q8 = tb_q8;
+            T.pk_p1 = ws.pk_p1; T.pk_b1 = ws.pk_b1; T.pk_ppb2 = ws.pk_ppb2;   // the launch's flag ranges
         }
         T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1;
         T.fb_list = T.fb_count = nullptr;
@@ -1183,6 +1213,14 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T.band = ws.band_fl.as<uint4>();
             T.band_w = pl.band_w; T.band_wd = pl.band_wd;
             T.pk_ppw = 2 * (64 / pl.G16);
+            if (T.pk_p1 != 0xFFFFFFFFu) {   // the second region of a mixed-shape launch (tail_shape)
+                const TailShape tail = tail_shape(pl, p, A, n);
+                if (!tail.fn || tail.p0 != T.pk_p1) { set_error("band traceback: tail shape changed"); return GASALX_EINVAL; }
+                T.band2 = A.bflags2;
+                T.band_wd2 = A.band_wd2;
+                T.pk_R2 = tail.R2; T.pk_G2 = tail.G2; T.pk_ppw2 = 2 * (64 / tail.G2);
+                T.pk_rmagic2 = (uint32_t)((0x100000000ull + tail.R2 - 1) / tail.R2);
+            }
             T.fb_count = fb_count;
             T.fb_list = fb_count + 64;
             HIPCHK(hipMemsetAsync(fb_count, 0, 4, st));
@@ -1211,6 +1249,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
             T2.n_dev = fb_count;
             T2.slot_of = nullptr;
             T2.pk_q8 = 0;
+            T2.pk_p1 = 0xFFFFFFFFu;   // the fallback launch is one shape (its n_dev excludes the tail)
             T2.fb_list = T2.fb_count = nullptr;
             tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T2);
             HIPCHK(hipGetLastError());

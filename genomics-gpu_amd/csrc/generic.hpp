@@ -590,6 +590,12 @@ struct TbArgs {
     // the CIGAR the full-matrix walk writes later)
     const uint4 *band;
     uint32_t band_w, band_wd, pk_ppw;   // pk_ppw: pairs (slots) per wave of the DP launch
+    // a mixed-shape DP launch (wf16_mix_kernel): slots from pk_p1 on ran the second shape (pk_G2 x
+    // pk_R2, band window band_wd2, buffers from band2 on), their flags from pk_b1 on, pk_ppb2 slots
+    // each (pk_p1 = 0xFFFFFFFF: one shape)
+    uint32_t pk_p1, pk_b1, pk_ppb2;
+    const uint4 *band2;
+    uint32_t band_wd2, pk_R2, pk_G2, pk_ppw2, pk_rmagic2;
     uint32_t *fb_list, *fb_count;
     // fallback walk: thread tid walks pair list[tid], tid < *n_dev; its slot in the DP launch is tid
     const uint32_t *list, *n_dev;
@@ -623,12 +629,16 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int i, j, total = 0, curr = 0;
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
     else { i = (int)tl; j = (int)ql; }
-    const bool pk = A.pk_flags && A.pk_flags[slot / A.pk_ppb];
+    const bool reg2 = slot >= A.pk_p1;   // the second shape of a mixed DP launch
+    const bool pk = A.pk_flags && A.pk_flags[reg2 ? A.pk_b1 + (slot - A.pk_p1) / A.pk_ppb2 : slot / A.pk_ppb];
     const bool bnd = pk && A.band;
-    // band layout: this pair's half of its lane group's entries in wave slot / pk_ppw
-    const uint2 *bnd2 = bnd ? reinterpret_cast<const uint2 *>(A.band) +
-                                  ((uint64_t)(slot / A.pk_ppw) * 64 + ((slot % A.pk_ppw) >> 1) * A.pk_G) *
-                                      ((A.band_wd / 4) * (A.pk_R / 4)) * 2 + (slot & 1u)
+    const uint32_t bslot = reg2 ? slot - A.pk_p1 : slot, bppw = reg2 ? A.pk_ppw2 : A.pk_ppw;
+    const uint32_t bG = reg2 ? A.pk_G2 : A.pk_G, bR = reg2 ? A.pk_R2 : A.pk_R;
+    const uint32_t bwd = reg2 ? A.band_wd2 : A.band_wd, bmagic = reg2 ? A.pk_rmagic2 : A.pk_rmagic;
+    // band layout: this pair's half of its lane group's entries in wave bslot / bppw
+    const uint2 *bnd2 = bnd ? reinterpret_cast<const uint2 *>(reg2 ? A.band2 : A.band) +
+                                  ((uint64_t)(bslot / bppw) * 64 + ((bslot % bppw) >> 1) * bG) * ((bwd / 4) * (bR / 4)) * 2 +
+                                  (slot & 1u)
                             : nullptr;
     bool out_of_band = false;
     // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
@@ -664,11 +674,11 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
             if (bnd) {
                 // band window of the row's lane: columns [L, L + wd), flags of 4 x 4 chunks
                 const uint32_t col = strip * 8 + c7;
-                const uint32_t lane = __umulhi(row, A.pk_rmagic), k = row - lane * A.pk_R;
-                const int32_t L = max((int32_t)(lane * A.pk_R) - (int32_t)A.band_w, 0);
+                const uint32_t lane = __umulhi(row, bmagic), k = row - lane * bR;
+                const int32_t L = max((int32_t)(lane * bR) - (int32_t)A.band_w, 0);
                 const uint32_t t = (uint32_t)((int32_t)col - L);
-                if (t >= A.band_wd) { out_of_band = true; break; }
-                const int64_t key = (((int64_t)lane * (A.band_wd / 4) + (t >> 2)) * (A.pk_R / 4) + (k >> 2)) * 2;
+                if (t >= bwd) { out_of_band = true; break; }
+                const int64_t key = (((int64_t)lane * (bwd / 4) + (t >> 2)) * (bR / 4) + (k >> 2)) * 2;
                 if (key != chunk_key) {
                     const uint2 c2 = bnd2[key];
                     chunk = make_uint4(c2.x, c2.y, 0u, 0u);

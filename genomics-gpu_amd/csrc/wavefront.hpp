@@ -62,6 +62,11 @@ struct WfArgs {
     uint2 *stm;
     uint4 *bflags;
     uint32_t band_w, band_wd;  // lane lg's window: columns [max(lg*R - band_w, 0), + band_wd), band_wd % 4 == 0
+    // a mixed-shape launch (wf16_mix_kernel): the second region's buffers and window width
+    uint32_t *cp2;
+    uint2 *stm2;
+    uint4 *bflags2;
+    uint32_t band_wd2;
     const uint32_t *n_dev;     // when set: the launch's pair count is *n_dev (<= n; traceback fallback list)
     const int32_t *lstop;      // LOCAL reverse pass of WITH_START (start.hpp): per pair the forward score; the
                                // e-drift sweep stops once every pair's first cell reaching it is settled

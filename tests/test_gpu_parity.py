@@ -1331,6 +1331,45 @@ def test_tail_shape_launch(engine, monkeypatch, kind, n, algo):
         assert np.array_equal(g0[f], o[f]), f
 
 
+@pytest.mark.parametrize("cp_tail", ["64", "32", "off"])
+def test_tail_shape_band_traceback(engine, monkeypatch, cp_tail):
+    """NW + CIGAR by band recomputation over more than two rounds of waves in one device call: the
+    last slots run the second shape (wf16_mix_kernel<WF16_GLOBAL_CP, 16, 20, 64, 8> or 32 x 12,
+    GASALX_CP_TAIL) with their own band buffers, and the walk (tb_kernel) reads each pair's band
+    flags with its region's shape.  Scores, CIGAR bytes and n_ops as the oracle; every pair packed."""
+    import torch
+    n = 60_000
+    b = G.Batch.synth(3, n, 0x7A31)
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
+    o = O.align(b, O.make_params(**kw))
+    monkeypatch.setenv("GASALX_TAIL", "0" if cp_tail == "off" else "1")
+    if cp_tail != "off":
+        monkeypatch.setenv("GASALX_CP_TAIL", cp_tail)
+    dev = torch.device("cuda", 0)
+    u = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32) if a.dtype == np.uint32 else a).to(dev)
+    d = {"q_batch": u(b.q_data), "t_batch": u(b.t_data), "q_offsets": u(b.q_offsets), "t_offsets": u(b.t_offsets),
+         "q_lens": u(b.q_lens), "t_lens": u(b.t_lens),
+         "aln_score": torch.full((n,), -7, dtype=torch.int32, device=dev),
+         "cigar": torch.zeros(b.q_bytes, dtype=torch.uint8, device=dev),
+         "n_cigar_ops": torch.zeros(n, dtype=torch.int32, device=dev)}
+    engine.packed_pairs()                                    # forget earlier launches
+    engine.align_device_ptrs(G.make_params(**kw), {k: v.data_ptr() for k, v in d.items()}, b.q_bytes, b.t_bytes,
+                             n, int(b.q_lens.max()), int(b.t_lens.max()))
+    torch.cuda.synchronize()
+    handled, total = engine.packed_pairs()
+    assert handled == total == n, (handled, total)
+    assert np.array_equal(d["aln_score"].cpu().numpy(), o["score"])
+    nops = d["n_cigar_ops"].cpu().numpy().view(np.uint32)
+    assert np.array_equal(nops, o["n_ops"]), int((nops != o["n_ops"]).sum())
+    # CIGAR bytes of the pairs whose CIGAR fits its slot (SURVEY Q14: longer ones overwrite the next)
+    got, ref = d["cigar"].cpu().numpy(), o["cigar"]
+    fits = o["n_ops"] <= (b.q_lens + 7) // 8 * 8
+    fits[1:] &= fits[:-1]                                    # and the pair before it did not run over
+    for i in np.nonzero(fits)[0][:: max(1, n // 4000)]:
+        s, k = int(b.q_offsets[i]), int(o["n_ops"][i])
+        assert np.array_equal(got[s:s + k], ref[s:s + k]), i
+
+
 @pytest.mark.parametrize("k_extra", ["0", "1"])
 def test_tail_shape_declined_blocks(engine, monkeypatch, k_extra):
     """IUPAC codes in pairs of both shapes' ranges: their blocks decline to the int32 kernel, which
