@@ -5,18 +5,22 @@
 # after them carry the traffic and issue-priced figures of this same library), smoke(), every bench
 # line (CPU baselines on the configs BASELINE.md quotes them for, the one-engine variants, the
 # drop-in boundary line), then kernel-trace summaries.  Output: gpurun_out/$FINAL_TAG (default
-# final)/, PMC copies in gpurun_out/final_pmc/.  SKIP_TESTS=1 / SKIP_PMC=1 leave those parts out.
-#   gpurun --timeout 1200 -- 'bash scripts/repro_final.sh'
+# final)/, PMC copies in gpurun_out/final_pmc/.  PARTS (default "tests pmc bench prof") picks the
+# parts, so the session fits gpurun's 20-minute limit in two or three calls:
+#   gpurun --timeout 1200 -- 'PARTS="tests pmc" bash scripts/repro_final.sh'
+#   gpurun --timeout 1200 -- 'PARTS="bench prof" bash scripts/repro_final.sh'
 set -u
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd $ROOT
 O=$ROOT/gpurun_out/${FINAL_TAG:-final}; mkdir -p $O $ROOT/gpurun_out/final_pmc
 fatal() { case $1 in 124|134|137|139) return 0;; *) return 1;; esac; }
-if [ "${SKIP_TESTS:-0}" != 1 ]; then
+PARTS=" ${PARTS:-tests pmc bench prof} "
+has() { case "$PARTS" in *" $1 "*) return 0;; *) return 1;; esac; }
+if has tests; then
   timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
   rc=$?; tail -1 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 fi
-if [ "${SKIP_PMC:-0}" != 1 ]; then
+if has pmc; then
   for wp in "sw_local 1000000" "pairhmm 100000" "semi 10000000" "nw_tb 100000" "sw_local_start 1000000" \
             "semi_start 10000000" "sw_local_300 1000000" "sw_local_tb 1000000" "nvbio_gotoh 262144" "semi_banded 10000000"; do
     set -- $wp
@@ -35,6 +39,7 @@ step() {  # step NAME SECONDS CMD...
   if fatal $rc; then echo "fatal in $name"; exit $rc; fi
   return 0
 }
+if has bench; then
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_default 600 python bench.py
 step bench_sw_local_start 600 python bench.py --workload sw_local_start --cpu-seconds 8
@@ -53,6 +58,8 @@ step bench_nvbio_gotoh 600 python bench.py --workload nvbio_gotoh --no-cpu
 step bench_nvbio_banded 600 python bench.py --workload nvbio_banded --no-cpu
 step bench_ksw 600 python bench.py --workload ksw --no-cpu
 step bench_boundary 600 python bench.py --workload boundary
+fi
+has prof || exit 0
 cd /tmp && export TMPDIR=/tmp
 for w in sw_local pairhmm semi semi_start sw_local_start sw_local_tb nw_tb; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$w -o run -- \
