@@ -373,7 +373,9 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 const bool seg_ok = frame && kseg_mode > 0 && mseg >= 2 && y8 <= 0xFFFF;
                 // key range: steps C + G (wavefront16.hpp step_local_dr: keys rank steps)
                 const int64_t kc = (int64_t)y8 + pl.G16;
-                if (frame && (hmax + 1) * kc <= 0x7800) {
+                // (GX_LOCAL_KA0: row k's keys carry e*k more, taken off after the sweep)
+                const int64_t hk = hmax + (GX_LOCAL_KA0 && !pl.tb ? e * (pl.R16 - 1) : 0);
+                if (frame && (hk + 1) * kc <= 0x7800) {
                     pl.kf16 = y8;
                 } else if (pl.tb) {
                     // (the traceback kernel has f16 keys only)
@@ -528,7 +530,8 @@ static TailShape tail_shape(const Plan &pl, const gasalx_params &p, const WfArgs
         const int64_t a = std::max(p.match, 0), e = p.gap_extend, oe = (int64_t)p.gap_open + e;
         const int64_t k = std::max<int64_t>(p.mismatch, p.has_n_penalty ? p.n_penalty : 0);
         const int64_t hmax = a * std::min(q8, y8), base = 0x400 + oe + k + 16;
-        if (!(base + hmax + e * span2 + a + k + 64 <= 0x7BFF && (hmax + 1) * (y8 + G2) <= 0x7800)) return t;
+        const int64_t hk2 = hmax + (GX_LOCAL_KA0 ? e * (R2 - 1) : 0);   // (KA0 key offsets)
+        if (!(base + hmax + e * span2 + a + k + 64 <= 0x7BFF && (hk2 + 1) * (y8 + G2) <= 0x7800)) return t;
         t.vmin = pl.vmin;
     } else {
         // the window offset for the larger span serves both shapes: their values then sit higher

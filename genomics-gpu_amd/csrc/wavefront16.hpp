@@ -98,6 +98,9 @@ constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_CP_ST16
 #define GX_CP_ST16 0       // A/B: the config-3 sweep's checkpoint and stream stores 16 bytes wide
 #endif
+#ifndef GX_LOCAL_KA0
+#define GX_LOCAL_KA0 1     // one key addend for every row (keys offset by e*k*M, taken off after the sweep): +0.6 %
+#endif
 #ifndef GX_LOCAL_ATIE
 #define GX_LOCAL_ATIE 1    // the LOCAL keys' scalar addends kept as a chain (with IL2: +2.4 %, profiles/r06/ab)
 #endif
@@ -216,7 +219,7 @@ __device__ __forceinline__ void step_local(const uint2 T, const int32_t c, const
 // two v_pk_max_u16 instead of one f16-pattern v_pk_maximum3 (one instruction more per two
 // cells), so (Hmax + 1) * C may reach 65536 instead of 0x7800: 150 bp at match 2, where the
 // round-3 planner fell back to the int32 kernel (2,627 GCUPS)
-template <int R, bool KEYS, bool U16 = false>
+template <int R, bool KEYS, bool U16 = false, bool KA0 = false>
 __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                               const uint32_t (&xs)[R], const uint32_t (&Hin)[R], uint32_t (&Hout)[R],
                                               uint32_t (&Ek)[R], uint32_t (&key)[R], uint32_t (&FL)[R],
@@ -250,18 +253,22 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                 key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H0, KMUL, a2)));
             else
                 key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H0, KMUL, a2));
-            a1 -= EM;
-            a2 -= EM;
+            if (!KA0) {
+                a1 -= EM;
+                a2 -= EM;
+            }
             if (U16)
                 key[k + 1] = pk_max_u16(key[k + 1], pk_max_u16(pk_mad_u16_lo(Hin[k + 1], KMUL, a1),
                                                                pk_mad_u16_lo(H1, KMUL, a2)));
             else
                 key[k + 1] = pk_max3(key[k + 1], pk_mad_u16_lo(Hin[k + 1], KMUL, a1), pk_mad_u16_lo(H1, KMUL, a2));
-            a1 -= EM;
-            a2 -= EM;
+            if (!KA0) {
+                a1 -= EM;
+                a2 -= EM;
 #if GX_LOCAL_ATIE
-            asm volatile("" : "+s"(a1), "+s"(a2));
+                asm volatile("" : "+s"(a1), "+s"(a2));
 #endif
+            }
         }
         FL[k] = pk_addnc(FL[k], EXT);
         FL[k + 1] = pk_addnc(FL[k + 1], EXT);
@@ -289,13 +296,15 @@ __device__ __forceinline__ void step_local_dr(const uint2 T, const uint32_t diag
                 key[k] = pk_max_u16(key[k], pk_max_u16(pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2)));
             else
                 key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
-            a1 -= EM;   // row k + 1: FL one e higher
-            a2 -= EM;
+            if (!KA0) {
+                a1 -= EM;   // row k + 1: FL one e higher
+                a2 -= EM;
 #if GX_LOCAL_ATIE
-            // keep the addends a chain of one subtract per row: left alone, the compiler rebuilt each
-            // row's from FL[k] (a subtract, a multiply and an add: 3 SALU per row instead of 1)
-            asm volatile("" : "+s"(a1), "+s"(a2));
+                // keep the addends a chain of one subtract per row: left alone, the compiler rebuilt each
+                // row's from FL[k] (a subtract, a multiply and an add: 3 SALU per row instead of 1)
+                asm volatile("" : "+s"(a1), "+s"(a2));
 #endif
+            }
         }
         FL[k] = pk_addnc(FL[k], EXT);
         f = pk_max_u16(toe, f);
