@@ -98,6 +98,9 @@ constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_CP_ST16
 #define GX_CP_ST16 0       // A/B: the config-3 sweep's checkpoint and stream stores 16 bytes wide
 #endif
+#ifndef GX_SEMI_PH4
+#define GX_SEMI_PH4 1      // the SEMI sweep's reset code only in its first G steps (+1.0 %)
+#endif
 #ifndef GX_LOCAL_KA0
 #define GX_LOCAL_KA0 1     // one key addend for every row (keys offset by e*k*M, taken off after the sweep): +0.6 %
 #endif
