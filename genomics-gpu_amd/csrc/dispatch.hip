@@ -635,7 +635,9 @@ static int launch_wavefront(Workspace &ws, const Plan &pl, const gasalx_params &
         A.skip_b1 = tail.b0;
         A.skip_ppb2 = tail.fn ? tail.ppb : 1;
     }
-    WfFn fn = A.stop ? wf_pick_stop(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb, pl.G, pl.R);
+    // (the band path's int32 launch aligns its declined blocks without direction words: the walk sends
+    // those pairs to the fallback list, whose launch writes them into the capped buffer)
+    WfFn fn = A.stop ? wf_pick_stop(pl.G, pl.R) : wf_lookup(pl.wf_algo, pl.keys, pl.tb && !pl.tb_band, pl.G, pl.R);
     if (!fn) { set_error("no wavefront instance"); return GASALX_EUNSUPPORTED; }
     if (pl.lds_bytes > 64 * 1024)
         HIPCHK(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds_bytes));
@@ -926,7 +928,11 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
     const bool wf_start = pl.kind == PLAN_WAVEFRONT && (p.algo == 3 || p.algo == 2) && p.start_pos == 1 &&
                           (out.q_start || out.t_start);
     // (whole groups of 8 pairs: the packed kernels' interleaved layout, tb_store_window)
-    if (runs_tb) HIPCHK(ws.tb.reserve((size_t)((n + 7) & ~7u) * tb_words * 4 + 64));
+    // the band path's full-matrix direction words serve its fallback list only: GASALX_TB_FBCAP slots
+    // (131,072 by default), the list then aligned in chunks of that many (the rest reserve every pair)
+    const uint32_t fb_cap = std::max(64, env_int("GASALX_TB_FBCAP", 131072));
+    const uint32_t n_tb = (pl.kind == PLAN_WAVEFRONT && pl.packed16 && pl.tb_band) ? std::min(n, fb_cap) : n;
+    if (runs_tb) HIPCHK(ws.tb.reserve((size_t)((n_tb + 7) & ~7u) * tb_words * 4 + 64));
     if (runs_tb || wf_start) {
         if ((p.algo == 3 || p.algo == 2) && (!qend || !tend)) {
             HIPCHK(ws.ends_q.reserve((size_t)n * 4));
@@ -1212,6 +1218,7 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         T.band = nullptr; T.band_w = 0; T.band_wd = 4; T.pk_ppw = 1;
         T.fb_list = T.fb_count = nullptr;
         T.list = T.n_dev = nullptr;
+        T.n_dev_off = 0; T.tb_slot = 0;
         if (fb_count) {
             T.band = ws.band_fl.as<uint4>();
             T.band_w = pl.band_w; T.band_wd = pl.band_wd;
@@ -1231,31 +1238,42 @@ static int align_body(Workspace &ws, const gasalx_params &p, const Plan &pl, con
         tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T);
         HIPCHK(hipGetLastError());
         if (fb_count) {
-            // pairs whose path left the band: the full-matrix packed traceback kernel over the
-            // list (slots = list positions; per-pair flag layout), its int32 kernel for any block
-            // it declines, and the walk again
+            // pairs whose path left the band (or whose block the packed launch declined): the
+            // full-matrix packed traceback kernel over the list (slots = list positions; per-pair
+            // flag layout at slot positions of the capped buffer), its int32 kernel for any block it
+            // declines, and the walk again -- in chunks of n_tb list positions, each launch reading
+            // the device-side count less its chunk's offset (empty chunks exit at once)
             Plan fp = pl;
             fp.tb_band = false;
-            WfArgs F = A;
-            // the band walk has written CIGAR prefixes over the query batch when that is the
-            // CIGAR buffer (get_tb.h:94): the DP reads align_device's copy of the codes then
-            if (walk_qseq) F.q = walk_qseq;
-            F.perm = T.fb_list;
-            F.n_dev = fb_count;
-            F.tb_q8 = 0;
-            F.cp = nullptr; F.stm = nullptr; F.bflags = nullptr;
-            int rc = launch_wavefront(ws, fp, p, F, st);
-            if (rc) return rc;
-            TbArgs T2 = T;
-            T2.band = nullptr;
-            T2.list = T.fb_list;
-            T2.n_dev = fb_count;
-            T2.slot_of = nullptr;
-            T2.pk_q8 = 0;
-            T2.pk_p1 = 0xFFFFFFFFu;   // the fallback launch is one shape (its n_dev excludes the tail)
-            T2.fb_list = T2.fb_count = nullptr;
-            tb_kernel<<<grid_for(n, 256), 256, 0, st>>>(T2);
-            HIPCHK(hipGetLastError());
+            for (uint32_t k0 = 0; k0 < n; k0 += n_tb) {
+                const uint32_t cn = std::min(n_tb, n - k0);
+                WfArgs F = A;
+                // the band walk has written CIGAR prefixes over the query batch when that is the
+                // CIGAR buffer (get_tb.h:94): the DP reads align_device's copy of the codes then
+                if (walk_qseq) F.q = walk_qseq;
+                F.perm = T.fb_list + k0;
+                F.n = cn;
+                F.n_dev = fb_count;
+                F.n_dev_off = k0;
+                F.tb_slot = 1;
+                F.tb_q8 = 0;
+                F.cp = nullptr; F.stm = nullptr; F.bflags = nullptr;
+                int rc = launch_wavefront(ws, fp, p, F, st);
+                if (rc) return rc;
+                TbArgs T2 = T;
+                T2.band = nullptr;
+                T2.list = T.fb_list + k0;
+                T2.n = cn;
+                T2.n_dev = fb_count;
+                T2.n_dev_off = k0;
+                T2.tb_slot = 1;
+                T2.slot_of = nullptr;
+                T2.pk_q8 = 0;
+                T2.pk_p1 = 0xFFFFFFFFu;   // the fallback launch is one shape (its n_dev excludes the tail)
+                T2.fb_list = T2.fb_count = nullptr;
+                tb_kernel<<<grid_for(cn, 256), 256, 0, st>>>(T2);
+                HIPCHK(hipGetLastError());
+            }
         }
     }
     return GASALX_OK;

@@ -597,8 +597,10 @@ struct TbArgs {
     const uint4 *band2;
     uint32_t band_wd2, pk_R2, pk_G2, pk_ppw2, pk_rmagic2;
     uint32_t *fb_list, *fb_count;
-    // fallback walk: thread tid walks pair list[tid], tid < *n_dev; its slot in the DP launch is tid
+    // fallback walk: thread t walks pair list[t], t < *n_dev - n_dev_off; its slot in the DP launch is t
+    // (tb_slot: its direction words at slot t of the capped buffer)
     const uint32_t *list, *n_dev;
+    uint32_t n_dev_off, tb_slot;
 };
 
 // 8 codes of a sequence cached per thread (the walk moves one position at a time)
@@ -619,12 +621,12 @@ __device__ __forceinline__ uint32_t pick4(const uint4 &c, uint32_t k) {
 
 __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t0 >= A.n || (A.n_dev && t0 >= *A.n_dev)) return;
+    if (t0 >= A.n || (A.n_dev && t0 + A.n_dev_off >= *A.n_dev)) return;
     const uint32_t tid = A.list ? A.list[t0] : t0;                          // the pair
     const uint32_t slot = A.list ? t0 : (A.slot_of ? A.slot_of[tid] : tid);   // its slot in the DP launch
     const uint32_t ql = A.qlen[tid], tl = A.tlen[tid];
     const uint32_t q8 = (ql + 7) & ~7u, tstrips = (tl + 7) >> 3;
-    const uint32_t *tb = A.tb + (uint64_t)tid * A.tb_pair_words;
+    const uint32_t *tb = A.tb + (uint64_t)(A.tb_slot ? slot : tid) * A.tb_pair_words;
     const int32_t OE = A.o + A.e;
     int i, j, total = 0, curr = 0;
     if (A.is_local) { i = A.tend[tid]; j = A.qend[tid]; total = A.score[tid]; }
@@ -640,7 +642,9 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
                                   ((uint64_t)(bslot / bppw) * 64 + ((bslot % bppw) >> 1) * bG) * ((bwd / 4) * (bR / 4)) * 2 +
                                   (slot & 1u)
                             : nullptr;
-    bool out_of_band = false;
+    // band path: the int32 kernel aligned a declined block's pairs without direction words (the
+    // fallback launch, over the list, writes them into the capped buffer)
+    bool out_of_band = A.band && !pk;
     // interleaved packed layout: the region of pairs (tid & ~7) .. (tid | 7), chunk c of this
     // pair at 8 * c + (tid & 7)
     const bool il8 = pk && A.pk_q8;
@@ -663,7 +667,7 @@ __global__ __launch_bounds__(256) void tb_kernel(TbArgs A) {
     int64_t chunk_key = -1;
     uint2 qv = make_uint2(0u, 0u), tv = make_uint2(0u, 0u);
     int32_t qkey = -1, tkey = -1;
-    while (i >= 0 && j >= 0) {
+    while (!out_of_band && i >= 0 && j >= 0) {
         // get_tb.h:50-71: linear cell index over (strip, row, column); a start
         // one row past the padded query (j == q8) wraps to row 0 of the next strip
         const bool wrap = j >= (int)q8;

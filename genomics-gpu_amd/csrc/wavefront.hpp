@@ -68,6 +68,8 @@ struct WfArgs {
     uint4 *bflags2;
     uint32_t band_wd2;
     const uint32_t *n_dev;     // when set: the launch's pair count is *n_dev (<= n; traceback fallback list)
+    uint32_t n_dev_off;        // ... less this offset (the fallback list in chunks of n slots)
+    uint32_t tb_slot;          // direction words indexed by slot, not by pair (the capped fallback buffer)
     const int32_t *lstop;      // LOCAL reverse pass of WITH_START (start.hpp): per pair the forward score; the
                                // e-drift sweep stops once every pair's first cell reaching it is settled
     // LOCAL keys by step segments (wavefront16.hpp WF16_LOCAL_SEG): segment j = steps [j*2^kseg_shift,
@@ -171,7 +173,7 @@ __device__ __forceinline__ uint32_t load4_codes_dir(const WfArgs &A, const uint8
 
 template <int ALGO, bool KEYS, bool TB, int G, int R, bool EXACT, bool STOP>
 __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, const uint32_t lg,
-                                        const uint32_t pair, const bool valid, const uint32_t ql,
+                                        const uint32_t pair, const uint32_t tbi, const bool valid, const uint32_t ql,
                                         const uint32_t tl, const uint32_t qpad, const uint32_t tpad,
                                         const uint32_t nsteps, const uint32_t (&qc)[R], const bool (&qn)[R]) {
     const int32_t OE = A.o + A.e;
@@ -300,7 +302,7 @@ __device__ __forceinline__ void wf_body(const WfArgs &A, const uint8_t *tcodes, 
                 }
             }
             if (TB && ((c & 7) == 7)) {
-                uint32_t *dst = A.tb + (uint64_t)pair * A.tb_pair_words + (uint64_t)(c >> 3) * qpad + r0;
+                uint32_t *dst = A.tb + (uint64_t)tbi * A.tb_pair_words + (uint64_t)(c >> 3) * qpad + r0;   // tbi: pair or slot
 #pragma unroll
                 for (int k = 0; k < R; k += 4) {
                     if (r0 + k < qpad) {
@@ -423,7 +425,8 @@ __device__ __forceinline__ void wf_block(const WfArgs &A, uint8_t *lds, const ui
     const uint32_t pair0 = (bx * kWavesPerBlock + wave) * P;
     const uint32_t idx = pair0 + slot;   // slot; the pair is perm[slot] when sorted
     // pairs the packed kernel already aligned are skipped (dispatch.hip); its flags are per block of slots
-    const uint32_t nn = A.n_dev ? min(*A.n_dev, A.n) : A.n;   // (traceback fallback: a device-side count)
+    // (traceback fallback: a device-side count, less the chunk's offset)
+    const uint32_t nn = A.n_dev ? min(*A.n_dev > A.n_dev_off ? *A.n_dev - A.n_dev_off : 0u, A.n) : A.n;
     const bool valid = idx < nn && !(A.skip && A.skip[skip_flag(A, idx)]);
     const uint32_t pair = (valid && A.perm) ? A.perm[idx] : idx;
     if (A.skip && !__syncthreads_or(valid)) return;      // block-uniform early exit
@@ -479,9 +482,11 @@ __device__ __forceinline__ void wf_block(const WfArgs &A, uint8_t *lds, const ui
     bool exact = A.force_exact != 0;
     if (ALGO != WF_GLOBAL || A.has_npen) exact = exact || __any(has_n);
     if (exact)
-        wf_body<ALGO, KEYS, TB, G, R, true, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+        wf_body<ALGO, KEYS, TB, G, R, true, STOP>(A, tcodes, lg, pair, A.tb_slot ? idx : pair, valid, ql, tl, qpad, tpad,
+                                                 nsteps, qc, qn);
     else
-        wf_body<ALGO, KEYS, TB, G, R, false, STOP>(A, tcodes, lg, pair, valid, ql, tl, qpad, tpad, nsteps, qc, qn);
+        wf_body<ALGO, KEYS, TB, G, R, false, STOP>(A, tcodes, lg, pair, A.tb_slot ? idx : pair, valid, ql, tl, qpad, tpad,
+                                                 nsteps, qc, qn);
 }
 
 // As the fallback of a packed launch (A.skip) the grid is capped (dispatch.hip wf_grid) and each

@@ -792,6 +792,23 @@ def test_global_traceback_band_and_fallback(engine, monkeypatch, w, n, lens):
     check(engine, no_cigar_overflow(b, **kw), cigar=True, **kw)
 
 
+@pytest.mark.parametrize("cap", ["64", "1000"])
+@pytest.mark.parametrize("w,alphabet", [("0", b"ACGT"), ("3", b"ACGTACGTACGTNR")])
+def test_global_traceback_band_capped_fallback(engine, monkeypatch, cap, w, alphabet):
+    """The band path's full-matrix direction buffer holds GASALX_TB_FBCAP slots, not one per pair:
+    the fallback list (paths that left the band, and pairs of blocks the packed launch declined,
+    whose int32 launch now writes no direction words) runs in chunks of that many list positions,
+    each launch reading the device-side count less its offset.  A narrow band sends most pairs
+    there; IUPAC codes decline blocks; uneven lengths run sorted slots."""
+    monkeypatch.setenv("GASALX_TB_BAND_W", w)
+    monkeypatch.setenv("GASALX_TB_FBCAP", cap)
+    kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
+    assert "_tbband_" in G.describe_plan(G.make_params(**kw), 300, 320)
+    b = rand_batch(zlib.crc32(repr((cap, w, alphabet)).encode()) & 0xFFFF, 5000, 100, 300, 60, 320,
+                   alphabet=alphabet)
+    check(engine, no_cigar_overflow(b, **kw), cigar=True, **kw)
+
+
 def test_global_traceback_band_equals_full_matrix(engine, monkeypatch):
     # config-3 data: the band pass + walk (+ fallback) and the full-matrix flags kernel agree
     kw = dict(algo=G.GLOBAL, start_pos=G.WITH_TB)
