@@ -374,7 +374,7 @@ Plan make_plan(const gasalx_params &p, const BatchShape &s, bool has_ops) {
                 // key range: steps C + G (wavefront16.hpp step_local_dr: keys rank steps)
                 const int64_t kc = (int64_t)y8 + pl.G16;
                 // (GX_LOCAL_KA0: row k's keys carry e*k more, taken off after the sweep)
-                const int64_t hk = hmax + (GX_LOCAL_KA0 && !pl.tb ? e * (pl.R16 - 1) : 0);
+                const int64_t hk = hmax + (GX_LOCAL_KA0 && (!pl.tb || GX_LTB_KA0) ? e * (pl.R16 - 1) : 0);
                 if (frame && (hk + 1) * kc <= 0x7800) {
                     pl.kf16 = y8;
                 } else if (pl.tb) {

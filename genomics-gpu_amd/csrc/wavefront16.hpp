@@ -101,6 +101,10 @@ constexpr int kW16_TB_WAVES = 2;   // GLOBAL + traceback kernel
 #ifndef GX_SEMI_PH4
 #define GX_SEMI_PH4 1      // the SEMI sweep's reset code only in its first G steps (+1.0 %)
 #endif
+#ifndef GX_LTB_KA0
+#define GX_LTB_KA0 1      // GX_LOCAL_KA0 in the LOCAL+TB kernel (step_local_tb_dr): 2,964 -> 3,144 GCUPS
+                          // (its two waves per SIMD issued the two scalar addend subtracts per row)
+#endif
 #ifndef GX_LOCAL_KA0
 #define GX_LOCAL_KA0 1     // one key addend for every row (keys offset by e*k*M, taken off after the sweep): +0.6 %
 #endif
@@ -410,7 +414,7 @@ __device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t m, uint32_t b) {
 // (step_local_dr), two columns per v_pk_maximum3 on the KEYS steps.  15.5 instructions per cell
 // pair instead of step_local_tb's 19.
 // ---------------------------------------------------------------------------
-template <int R, bool KEYS>
+template <int R, bool KEYS, bool KA0 = false>
 __device__ __forceinline__ void step_local_tb_dr(const uint2 T, const uint32_t diag_top, const uint32_t f_top,
                                                  const uint32_t (&xs)[R], const uint32_t (&Hin)[R],
                                                  uint32_t (&Hout)[R], uint32_t (&Ek)[R], uint32_t (&key)[R],
@@ -434,14 +438,16 @@ __device__ __forceinline__ void step_local_tb_dr(const uint2 T, const uint32_t d
         dw[k] = and_or(m2, M2, j == 0 ? (m1 & M1) : and_or(m1, M1, dw[k]));
         if (KEYS) {
             key[k] = pk_max3(key[k], pk_mad_u16_lo(Hin[k], KMUL, a1), pk_mad_u16_lo(H, KMUL, a2));
-            a1 -= EM;
-            a2 -= EM;
+            if (!KA0) {
+                a1 -= EM;
+                a2 -= EM;
+            }
         }
         flk = pk_addnc(flk, EXT);
         Ek[k] = En;
         f = Fn;
         Hout[k] = H;
-        if (KEYS) asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(a1), "+s"(a2), "+s"(flk));
+        if (KEYS && !KA0) asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(a1), "+s"(a2), "+s"(flk));
         else asm volatile("" : "+v"(dw[k]), "+v"(f), "+s"(flk));
     };
 #if GX_TB_IL2
